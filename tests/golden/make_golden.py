@@ -1,0 +1,310 @@
+"""Generate golden fixtures from the reference's OWN Python code (run in the dev container only).
+
+    python -O tests/golden/make_golden.py   # -O = PYTHONOPTIMIZE, required by the reference (README.md:28)
+
+The reference is imported from /root/reference behind the stubs in ``refstubs.py`` (cvxpy
+tracing layer answered by the oracle IPM, closed-form pinocchio, oracle geometry for hppfcl,
+inert meshcat/polytope).  Everything written here is *data*: inputs and the reference code's
+outputs, as small .npz files next to this script.  Nothing of the reference's source travels.
+
+What each fixture pins (reference file:line):
+  ref_params.npz      RQPParameters + f_eq + controller constants   system/rigid_quadrotor_payload.py:48-84,
+                                                                    control/rqp_cadmm.py:142-236
+  ref_dynamics.npz    forward_dynamics, inverse_dynamics_error, RQPState.integrate/project_R
+                                                                    system/rigid_quadrotor_payload.py:121-269
+  ref_lowlevel.npz    RQPLowLevelController("pd").control          control/rqp_centralized.py:457-535
+  ref_forest.npz      Forest() tree layouts for np.random.seed(0..3) example/env_forest.py:47-85
+  ref_env_rows.npz    _set_collision_avoidance_cbf_parameters       control/rqp_cadmm.py:307-373,
+                                                                    control/rqp_centralized.py:280-337
+  ref_qp.npz          the conic problem data cvxpy would receive    control/rqp_*.py constraint/cost builders
+  ref_cadmm.npz       RQPCADMMController.control sequences          control/rqp_cadmm.py:631-675
+  ref_dd.npz          RQPDDController.control sequences             control/rqp_dd.py:695-752
+  ref_central.npz     RQPCentralizedController.control              control/rqp_centralized.py:436-448
+  ref_closed_loop.npz rqp_example-style closed loop (HL every 10)   example/rqp_example.py:120-131
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+import refstubs  # noqa: E402
+
+refstubs.install()
+sys.path.insert(0, REF)
+
+from control.rqp_cadmm import RQPCADMMController  # noqa: E402
+from control.rqp_centralized import RQPCentralizedController, RQPLowLevelController  # noqa: E402
+from control.rqp_dd import RQPDDController  # noqa: E402
+from example.env_forest import Forest  # noqa: E402
+from example.setup import rqp_setup  # noqa: E402
+from system.rigid_quadrotor_payload import RQPDynamics, RQPParameters, RQPState  # noqa: E402
+
+from oracle.model import exp3  # noqa: E402
+
+OUT = HERE
+
+
+def rand_rot(rng, scale):
+    return exp3(rng.uniform(-scale, scale, 3))
+
+
+def rand_state(rng, n, big=False):
+    R = np.stack([rand_rot(rng, 0.3 if not big else 1.0) for _ in range(n)], axis=2)
+    w = rng.uniform(-0.5, 0.5, (3, n))
+    xl = rng.uniform(-1, 1, 3)
+    vl = rng.uniform(-0.5, 0.5, 3)
+    Rl = rand_rot(rng, 0.1 if not big else 0.5)
+    wl = rng.uniform(-0.2, 0.2, 3)
+    return RQPState(R, w, xl, vl, Rl, wl)
+
+
+def pack_state(s):
+    return dict(R=s.R.copy(), w=s.w.copy(), xl=s.xl.copy(), vl=s.vl.copy(), Rl=s.Rl.copy(), wl=s.wl.copy())
+
+
+def stack_states(states):
+    return {k: np.stack([st[k] for st in states]) for k in states[0]}
+
+
+def gen_params():
+    p, col, s0 = rqp_setup(3)
+    ctrl = RQPCADMMController(p, col, s0, 1e-3)
+    ps = ctrl.primal_solvers[0]
+    np.savez(os.path.join(OUT, "ref_params.npz"), mT=p.mT, x_com=p.x_com, r_com=p.r_com, JT=p.JT,
+             JT_inv=p.JT_inv, f_eq=ps.f_eq, col_radius=col.collision_radius,
+             max_deceleration=col.max_deceleration, min_fz=ps.min_fz, max_f=ps.max_f,
+             vision_radius=ps.vision_radius, sec_max_f_ang=ps.sec_max_f_ang)
+
+
+def gen_dynamics():
+    rng = np.random.default_rng(7)
+    out = {}
+    for n, tag in ((3, "n3"), (4, "n4")):
+        if n == 3:
+            p, _, _ = rqp_setup(3)
+        else:
+            r = rng.uniform(-1, 1, (3, n))
+            J = np.stack([np.diag([2.32, 2.32, 4]) * 1e-3] * n, axis=2)
+            p = RQPParameters(np.full(n, 0.5), J, 0.225, np.diag([2.1, 1.87, 3.97]) * 1e-2, r)
+        states, wr_f, wr_M, dws, dvls, dwls, errs = [], [], [], [], [], [], []
+        for _ in range(16):
+            s = rand_state(rng, n, big=True)
+            f = rng.random(n) * p.mT * 9.80665 / n
+            M = rng.random((3, n)) - 0.5
+            dyn = RQPDynamics(p, s, 1e-3)
+            dw, dvl, dwl = dyn.forward_dynamics((f, M))
+            states.append(pack_state(s))
+            wr_f.append(f), wr_M.append(M), dws.append(dw), dvls.append(dvl), dwls.append(dwl)
+            errs.append(RQPDynamics.inverse_dynamics_error(s, p, (f, M), (dw, dvl, dwl)))
+        st = stack_states(states)
+        for k, v in st.items():
+            out[f"{tag}_fd_{k}"] = v
+        out[f"{tag}_fd_f"], out[f"{tag}_fd_M"] = np.array(wr_f), np.array(wr_M)
+        out[f"{tag}_fd_dw"], out[f"{tag}_fd_dvl"], out[f"{tag}_fd_dwl"] = np.array(dws), np.array(dvls), np.array(dwls)
+        out[f"{tag}_fd_err"] = np.array(errs)
+        out[f"{tag}_r"], out[f"{tag}_m"], out[f"{tag}_J"] = p.r, p.m, p.J
+        out[f"{tag}_ml"], out[f"{tag}_Jl"] = p.ml, p.Jl
+        # integration: 45 steps of dt = 5e-3 with random wrenches (crosses two projections)
+        s = rand_state(rng, n, big=True)
+        out[f"{tag}_int_s0"] = np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl])
+        dyn = RQPDynamics(p, s, 5e-3)
+        fs, Ms = [], []
+        for _ in range(45):
+            f = rng.random(n) * p.mT * 9.80665 / n
+            M = (rng.random((3, n)) - 0.5) * 0.01
+            fs.append(f), Ms.append(M)
+            dyn.integrate((f, M))
+        out[f"{tag}_int_f"], out[f"{tag}_int_M"] = np.array(fs), np.array(Ms)
+        s = dyn.state
+        out[f"{tag}_int_s1"] = np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl])
+    np.savez(os.path.join(OUT, "ref_dynamics.npz"), **out)
+
+
+def gen_lowlevel():
+    rng = np.random.default_rng(11)
+    p, _, _ = rqp_setup(3)
+    ll = RQPLowLevelController("pd", p, np.pi / 6)
+    states, fdes, fs, Ms = [], [], [], []
+    for _ in range(16):
+        s = rand_state(rng, 3, big=True)
+        fd = np.vstack([rng.uniform(-2, 2, (2, 3)), rng.uniform(3, 8, (1, 3))])
+        f, M = ll.control(s, fd)
+        states.append(pack_state(s)), fdes.append(fd), fs.append(f), Ms.append(M)
+    np.savez(os.path.join(OUT, "ref_lowlevel.npz"), **{f"s_{k}": v for k, v in stack_states(states).items()},
+             f_des=np.array(fdes), f=np.array(fs), M=np.array(Ms))
+
+
+def gen_forest():
+    out = {}
+    for seed in range(4):
+        np.random.seed(seed)
+        env = Forest()
+        out[f"tree_pos_{seed}"] = env.tree_pos
+    out["mountain_sphere_radius"] = env.mountain_sphere_radius
+    out["mountain_center_depth"] = env.mountain_center_depth
+    np.savez(os.path.join(OUT, "ref_forest.npz"), **out)
+
+
+def forest_state(rng, env, n):
+    # payload heading through the forest: pick a tree and start 2-5 m in front of it
+    k = rng.integers(env.num_trees)
+    tp = env.tree_pos[k]
+    ang = rng.uniform(-0.4, 0.4)
+    dist = rng.uniform(1.6, 4.0)
+    xl = np.array([tp[0] - dist * np.cos(ang), tp[1] - dist * np.sin(ang), tp[2] + rng.uniform(-1.5, 2.5)])
+    vl = np.array([rng.uniform(0.2, 0.9), rng.uniform(-0.3, 0.3), rng.uniform(-0.1, 0.1)])
+    R = np.stack([rand_rot(rng, 0.2) for _ in range(n)], axis=2)
+    return RQPState(R, rng.uniform(-0.3, 0.3, (3, n)), xl, vl, rand_rot(rng, 0.1), rng.uniform(-0.1, 0.1, 3))
+
+
+def gen_env_rows():
+    np.random.seed(0)
+    env = Forest()
+    rng = np.random.default_rng(5)
+    p, col, s0 = rqp_setup(3)
+    cad = RQPCADMMController(p, col, s0, 1e-3, env)
+    cen = RQPCentralizedController(p, col, s0, 1e-3, env)
+    states, lhs_d, rhs_d, col_d, md_d, lhs_c, rhs_c, col_c, md_c = [], [], [], [], [], [], [], [], []
+    for _ in range(24):
+        s = forest_state(rng, env, 3)
+        states.append(pack_state(s))
+        L, Rr, C, Md = [], [], [], []
+        for i in range(3):
+            ps = cad.primal_solvers[i]
+            ps._set_collision_avoidance_cbf_parameters(s)
+            L.append(ps.env_cbf_lhs.value.copy()), Rr.append(ps.env_cbf_rhs.value.copy())
+            C.append(ps.collision), Md.append(ps.min_env_dist)
+        lhs_d.append(L), rhs_d.append(Rr), col_d.append(C), md_d.append(Md)
+        cen._set_collision_avoidance_cbf_parameters(s)
+        lhs_c.append(cen.env_cbf_lhs.value.copy()), rhs_c.append(cen.env_cbf_rhs.value.copy())
+        col_c.append(cen.collision), md_c.append(cen.min_env_dist)
+    np.savez(os.path.join(OUT, "ref_env_rows.npz"), **{f"s_{k}": v for k, v in stack_states(states).items()},
+             tree_pos=env.tree_pos, lhs_d=np.array(lhs_d), rhs_d=np.array(rhs_d), col_d=np.array(col_d),
+             md_d=np.array(md_d), lhs_c=np.array(lhs_c), rhs_c=np.array(rhs_c), col_c=np.array(col_c),
+             md_c=np.array(md_c))
+
+
+def gen_qp():
+    """Trace the exact problems the reference builds (no env; env rows are pinned separately)."""
+    rng = np.random.default_rng(3)
+    p, col, s0 = rqp_setup(3)
+    out = {}
+    cad = RQPCADMMController(p, col, s0, 1e-3)
+    dd = RQPDDController(p, col, s0, 1e-3)
+    cen = RQPCentralizedController(p, col, s0, 1e-3)
+    for case in range(6):
+        s = rand_state(rng, 3)
+        acc = (rng.uniform(-2, 2, 3), rng.uniform(-2, 2, 3))
+        i = case % 3
+        lam = rng.normal(0, 0.5, (3, 3))
+        fm = rng.normal(0, 2, (3, 3)) + cad.primal_solvers[0].f_eq
+        refstubs.TRACE.clear()
+        cad.primal_solvers[i].solve(s, acc, lam, 1.0, fm)
+        t = refstubs.TRACE[-1]
+        pre = f"cadmm{case}_"
+        for k in ("P", "q", "A", "b", "G", "h", "l", "q_dims", "x"):
+            out[pre + k] = t[k]
+        out[pre + "i"], out[pre + "lam"], out[pre + "fm"] = i, lam, fm
+        out[pre + "acc"] = np.concatenate(acc)
+        for k, v in pack_state(s).items():
+            out[pre + "s_" + k] = v
+        cf, cF, cM = rng.normal(0, 1, 3), rng.normal(0, 1, 3), rng.normal(0, 0.3, 3)
+        refstubs.TRACE.clear()
+        dd.primal_solvers[i].solve(s, acc, cf, cF, cM)
+        t = refstubs.TRACE[-1]
+        pre = f"dd{case}_"
+        for k in ("P", "q", "A", "b", "G", "h", "l", "q_dims", "x"):
+            out[pre + k] = t[k]
+        out[pre + "i"], out[pre + "c"] = i, np.concatenate([cf, cF, cM])
+        out[pre + "acc"] = np.concatenate(acc)
+        for k, v in pack_state(s).items():
+            out[pre + "s_" + k] = v
+        refstubs.TRACE.clear()
+        cen.control(s, acc)
+        t = refstubs.TRACE[-1]
+        pre = f"cen{case}_"
+        for k in ("P", "q", "A", "b", "G", "h", "l", "q_dims", "x"):
+            out[pre + k] = t[k]
+        out[pre + "acc"] = np.concatenate(acc)
+        for k, v in pack_state(s).items():
+            out[pre + "s_" + k] = v
+    np.savez(os.path.join(OUT, "ref_qp.npz"), **out)
+
+
+def gen_outer_loops():
+    """_plot_convergence_rate recipe (test/control/test_rqpcontrollers.py:101-124) + default tolerance."""
+    p, col, s0 = rqp_setup(3)
+    np.random.seed(0)
+    accs = [((np.random.random(3) - 0.5) * 10.0, (np.random.random(3) - 0.5) * 10.0) for _ in range(6)]
+    for name, cls in (("cadmm", RQPCADMMController), ("dd", RQPDDController)):
+        out = {"acc": np.array([np.concatenate(a) for a in accs])}
+        c = cls(p, col, s0, 1e-3)
+        if name == "cadmm":
+            c.set_force_err_tolerance(0.0, False)
+        else:
+            c.set_force_err_tolerance(0.0)
+        c.set_max_iter(25)
+        errs, fs = [], []
+        for a in accs[:3]:
+            f, st = c.control(s0, a)
+            errs.append(st.err_seq), fs.append(f.copy())
+        out["fixed_err"], out["fixed_f"] = np.array(errs), np.array(fs)
+        c = cls(p, col, s0, 1e-3)
+        its, fs, errs = [], [], []
+        for a in accs:
+            f, st = c.control(s0, a)
+            its.append(st.iter), fs.append(f.copy()), errs.append(np.pad(np.array(st.err_seq, float), (0, 101 - len(st.err_seq)), constant_values=np.nan))
+        out["tol_iters"], out["tol_f"], out["tol_err"] = np.array(its), np.array(fs), np.array(errs)
+        np.savez(os.path.join(OUT, f"ref_{name}.npz"), **out)
+    c = RQPCentralizedController(p, col, s0, 1e-3)
+    fs = [c.control(s0, a)[0].copy() for a in accs]
+    np.savez(os.path.join(OUT, "ref_central.npz"), acc=np.array([np.concatenate(a) for a in accs]), f=np.array(fs))
+
+
+def gen_closed_loop(steps=400):
+    """rqp_example main loop (example/rqp_example.py:120-131): forest seed 0, HL every 10 steps."""
+    out = {}
+    for name in ("consensus-admm", "dual-decomposition", "centralized"):
+        np.random.seed(0)
+        env = Forest()
+        p, col, s0 = rqp_setup(3)
+        dyn = RQPDynamics(p, s0, 1e-3)
+        cls = {"consensus-admm": RQPCADMMController, "dual-decomposition": RQPDDController,
+               "centralized": RQPCentralizedController}[name]
+        hl = cls(p, col, s0, 1e-3, env)
+        ll = RQPLowLevelController("pd", p, hl.get_force_cone_angle_bound())
+        from example.rqp_example import _desired_acceleration_forest  # noqa: E402 (matplotlib import)
+        fdes, its, xs, mds = [], [], [], []
+        for i in range(steps):
+            if i % 10 == 0:
+                acc, _, _ = _desired_acceleration_forest(dyn.state, i * 1e-3, env)
+                f_des, st = hl.control(dyn.state, acc)
+                fdes.append(f_des.copy()), its.append(st.iter), mds.append(st.min_env_dist)
+            w = ll.control(dyn.state, f_des)
+            dyn.integrate(w)
+            s = dyn.state
+            xs.append(np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl]))
+        tag = name.split("-")[0][:4]
+        out[f"{tag}_f_des"], out[f"{tag}_iters"] = np.array(fdes), np.array(its)
+        out[f"{tag}_states"], out[f"{tag}_min_dist"] = np.array(xs), np.array(mds)
+    np.savez(os.path.join(OUT, "ref_closed_loop.npz"), **out)
+
+
+if __name__ == "__main__":
+    import time
+
+    for fn in (gen_params, gen_dynamics, gen_lowlevel, gen_forest, gen_env_rows, gen_qp, gen_outer_loops,
+               gen_closed_loop):
+        t = time.time()
+        fn()
+        print(f"{fn.__name__}: {time.time() - t:.1f}s", flush=True)
