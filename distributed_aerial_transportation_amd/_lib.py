@@ -1,0 +1,124 @@
+"""ctypes binding of libdat.so (the C-ABI in include/dat.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is visible,
+the controllers raise.  ``build()`` compiles the library in-tree for gfx950 with hipcc.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libdat.so")
+SRC = os.path.join(PKG, "csrc", "dat.hip")
+DEPS = [SRC, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_layout.h"),
+        os.path.join(REPO, "include", "dat.h")]
+
+MODE_CENTRALIZED, MODE_CADMM, MODE_DD = 0, 1, 2
+QP_OPTIMAL, QP_INACCURATE, QP_INFEASIBLE, QP_FAILED = 0, 1, 2, 3
+
+
+class DatError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("mode", ctypes.c_int),
+        ("n", ctypes.c_int),
+        ("batch", ctypes.c_int),
+        ("dt", ctypes.c_double),
+        ("hl_every", ctypes.c_int),
+        ("max_iter", ctypes.c_int),
+        ("res_tol", ctypes.c_double),
+        ("use_total_res", ctypes.c_int),
+        ("rho0", ctypes.c_double),
+        ("tau_incr", ctypes.c_double),
+        ("rho_max", ctypes.c_double),
+        ("record_err", ctypes.c_int),
+    ]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libdat.so (gfx950) next to this file if it is missing or stale."""
+    stale = not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(d) for d in DEPS)
+    if force or stale:
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", SRC, "-o", LIB_PATH]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise DatError("hipcc failed:\n" + r.stderr[-4000:])
+        if verbose:
+            print(" ".join(cmd))
+    return LIB_PATH
+
+
+_lib = None
+
+D = ctypes.POINTER(ctypes.c_double)
+I = ctypes.POINTER(ctypes.c_int)
+U8 = ctypes.POINTER(ctypes.c_uint8)
+LL = ctypes.POINTER(ctypes.c_longlong)
+H = ctypes.c_void_p
+
+EXPORTS = {
+    "dat_default_config": (None, [ctypes.POINTER(Config)]),
+    "dat_create": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(H)]),
+    "dat_destroy": (ctypes.c_int, [H]),
+    "dat_last_error": (ctypes.c_char_p, []),
+    "dat_device_count": (ctypes.c_int, []),
+    "dat_set_params": (ctypes.c_int, [H, D, ctypes.c_int]),
+    "dat_set_forests": (ctypes.c_int, [H, ctypes.c_int, I, D, I, D]),
+    "dat_set_tolerance": (ctypes.c_int, [H, ctypes.c_double, ctypes.c_int]),
+    "dat_set_max_iter": (ctypes.c_int, [H, ctypes.c_int]),
+    "dat_reset_warm_start": (ctypes.c_int, [H]),
+    "dat_set_state": (ctypes.c_int, [H, D, I]),
+    "dat_get_state": (ctypes.c_int, [H, D, I]),
+    "dat_control_step": (ctypes.c_int, [H, D, D, D, I, I, D, U8, D]),
+    "dat_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
+    "dat_closed_loop": (ctypes.c_int, [H, ctypes.c_int]),
+    "dat_get_counters": (ctypes.c_int, [H, LL, LL, LL, D]),
+    "dat_reset_counters": (ctypes.c_int, [H]),
+    "dat_synchronize": (ctypes.c_int, [H]),
+    "dat_env_rows": (ctypes.c_int, [H, D, D, I, U8, D]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load libdat.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DatError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise DatError(lib().dat_last_error().decode())
+
+
+def ptr(a, ctype=D):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctype)
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)

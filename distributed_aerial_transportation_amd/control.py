@@ -1,0 +1,282 @@
+"""Controllers on top of libdat.so -- the reference's controller API, batched and drop-in.
+
+Batched engine
+  ``BatchedController(mode, n, batch, params, col, ...)``: one HIP handle driving B independent
+  scenarios; ``control(states, acc_des)`` runs one high-level step for all of them on the GPU.
+
+Drop-in single-scenario classes (same constructor and per-step interface as the reference):
+  ``RQPCentralizedController``  control/rqp_centralized.py:27-455
+  ``RQPCADMMController``        control/rqp_cadmm.py:510-688
+  ``RQPDDController``           control/rqp_dd.py:558-764
+  each: ``__init__(params, col, state, dt, env=None, verbose=False)``,
+        ``control(state, acc_des) -> (f_des (3, n), SolverStatistics)``,
+        ``get_force_cone_angle_bound()``, ``get_dist_eps()``,
+        ``set_force_err_tolerance(tol[, use_total_res])``, ``set_max_iter(k)`` (C-ADMM / DD).
+  ``RQPLowLevelController`` / ``RQPDynamics``: low-level PD + rigid-body rollout on the GPU.
+The QPs are solved by the HIP kernels; the reference's Clarabel per-call solve time becomes the
+GPU kernel time of the step (``SolverStatistics.solve_time``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Any, List, Optional
+
+import numpy as np
+
+from . import _lib as L
+from . import layout
+from .system import RQPCollision, RQPParameters, RQPState, pack_mountain, pack_params, pack_state
+
+MODES = {"centralized": L.MODE_CENTRALIZED, "consensus-admm": L.MODE_CADMM, "cadmm": L.MODE_CADMM,
+         "dual-decomposition": L.MODE_DD, "dd": L.MODE_DD}
+
+
+@dataclass
+class SolverStatistics:
+    """control/rqp_centralized.py:18-24."""
+
+    iter: int
+    solve_time: float
+    collision: bool
+    min_env_dist: float
+    err_seq: Optional[List[float]] = None
+
+
+@dataclass
+class StepResult:
+    """Batched outputs of one high-level step (leading axis: scenario)."""
+
+    f_des: np.ndarray           # (B, 3, n)
+    iters: np.ndarray           # (B,)
+    qp_status: np.ndarray       # (B, n)
+    min_env_dist: np.ndarray    # (B,)
+    collision: np.ndarray       # (B,) bool
+    err_seq: Optional[np.ndarray] = None  # (B, max_iter + 1), NaN padded
+    gpu_ms: float = 0.0
+
+
+class BatchedController:
+    """B independent scenarios of one controller type on one GPU."""
+
+    def __init__(self, mode, n: int, batch: int, params: np.ndarray, *, per_scenario_params: bool = False,
+                 dt: float = 1e-3, hl_every: int = 10, device: int = 0, max_iter: int = 100, res_tol: float = 1e-2,
+                 use_total_res: bool = True, record_err: bool = False, rho0: float = 1.0, tau_incr: float = 1.0,
+                 rho_max: float = 2.0) -> None:
+        self.mode = MODES[mode] if isinstance(mode, str) else int(mode)
+        self.n, self.batch = n, batch
+        lib = L.lib()
+        cfg = L.Config()
+        lib.dat_default_config(cfg)
+        cfg.device, cfg.mode, cfg.n, cfg.batch = device, self.mode, n, batch
+        cfg.dt, cfg.hl_every, cfg.max_iter, cfg.res_tol = dt, hl_every, max_iter, res_tol
+        cfg.use_total_res, cfg.record_err = int(use_total_res), int(record_err)
+        cfg.rho0, cfg.tau_incr, cfg.rho_max = rho0, tau_incr, rho_max
+        self.cfg = cfg
+        h = L.H()
+        L.check(lib.dat_create(cfg, h))
+        self._h = h
+        self._lib = lib
+        params = L.f64(params)
+        if per_scenario_params:
+            assert params.shape == (batch, layout.param_size(n)), params.shape
+        else:
+            assert params.shape == (layout.param_size(n),), params.shape
+        self.params = params
+        L.check(lib.dat_set_params(h, L.ptr(params), int(per_scenario_params)))
+
+    # -- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.dat_destroy(self._h)
+            self._h = None
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+    # -- configuration
+    def set_forests(self, forests: list, scenario_forest: Optional[np.ndarray] = None) -> None:
+        """forests: list of objects with tree_pos (T, 3) and mountain constants; [] removes the env."""
+        if not forests:
+            L.check(self._lib.dat_set_forests(self._h, 0, None, None, None, None))
+            return
+        offs = np.zeros(len(forests) + 1, dtype=np.int32)
+        for k, f in enumerate(forests):
+            offs[k + 1] = offs[k] + f.tree_pos.shape[0]
+        trees = L.f64(np.concatenate([f.tree_pos for f in forests]))
+        mountains = L.f64(np.stack([pack_mountain(f) for f in forests]))
+        sf = None if scenario_forest is None else L.i32(scenario_forest)
+        if sf is not None:
+            assert sf.shape == (self.batch,)
+        L.check(self._lib.dat_set_forests(self._h, len(forests), L.ptr(offs, L.I), L.ptr(trees),
+                                          None if sf is None else L.ptr(sf, L.I), L.ptr(mountains)))
+
+    def set_force_err_tolerance(self, tol: float, use_total_res: bool = True) -> None:
+        L.check(self._lib.dat_set_tolerance(self._h, float(tol), int(use_total_res)))
+        self.cfg.res_tol, self.cfg.use_total_res = tol, int(use_total_res)
+
+    def set_max_iter(self, max_iter: int) -> None:
+        L.check(self._lib.dat_set_max_iter(self._h, int(max_iter)))
+        self.cfg.max_iter = max_iter
+
+    def reset_warm_start(self) -> None:
+        L.check(self._lib.dat_reset_warm_start(self._h))
+
+    # -- state
+    def set_state(self, states: np.ndarray, counters: Optional[np.ndarray] = None) -> None:
+        states = L.f64(states)
+        assert states.shape == (self.batch, layout.state_size(self.n))
+        c = None if counters is None else L.i32(counters)
+        L.check(self._lib.dat_set_state(self._h, L.ptr(states), None if c is None else L.ptr(c, L.I)))
+
+    def get_state(self):
+        st = np.empty((self.batch, layout.state_size(self.n)))
+        c = np.empty(self.batch, dtype=np.int32)
+        L.check(self._lib.dat_get_state(self._h, L.ptr(st), L.ptr(c, L.I)))
+        return st, c
+
+    # -- steps
+    def control(self, states: Optional[np.ndarray] = None, acc_des: Optional[np.ndarray] = None) -> StepResult:
+        B, n = self.batch, self.n
+        st = None if states is None else L.f64(states)
+        acc = None if acc_des is None else L.f64(acc_des)
+        if st is not None:
+            assert st.shape == (B, layout.state_size(n))
+        if acc is not None:
+            assert acc.shape == (B, 6)
+        f = np.empty((B, 3 * n))
+        it = np.empty(B, dtype=np.int32)
+        qs = np.empty((B, n), dtype=np.int32)
+        md = np.empty(B)
+        col = np.empty(B, dtype=np.uint8)
+        err = np.empty((B, self.cfg.max_iter + 1)) if self.cfg.record_err else None
+        _, _, _, ms0 = self.counters()
+        L.check(self._lib.dat_control_step(self._h, L.ptr(st), L.ptr(acc), L.ptr(f), L.ptr(it, L.I), L.ptr(qs, L.I),
+                                           L.ptr(md), L.ptr(col, L.U8), L.ptr(err)))
+        _, _, _, ms1 = self.counters()
+        return StepResult(f.reshape(B, n, 3).transpose(0, 2, 1), it, qs, md, col.astype(bool), err, ms1 - ms0)
+
+    def rollout(self, steps: int, f_des: Optional[np.ndarray] = None) -> None:
+        fd = None
+        if f_des is not None:
+            fd = L.f64(np.asarray(f_des).transpose(0, 2, 1).reshape(self.batch, 3 * self.n))
+        L.check(self._lib.dat_rollout(self._h, int(steps), L.ptr(fd)))
+
+    def closed_loop(self, hl_steps: int) -> None:
+        L.check(self._lib.dat_closed_loop(self._h, int(hl_steps)))
+
+    def env_rows(self):
+        B, n = self.batch, self.n
+        lhs = np.empty((B, n, layout.NENV, 3))
+        rhs = np.empty((B, n, layout.NENV))
+        nr = np.empty((B, n), dtype=np.int32)
+        col = np.empty((B, n), dtype=np.uint8)
+        md = np.empty((B, n))
+        L.check(self._lib.dat_env_rows(self._h, L.ptr(lhs), L.ptr(rhs), L.ptr(nr, L.I), L.ptr(col, L.U8), L.ptr(md)))
+        return lhs, rhs, nr, col.astype(bool), md
+
+    def counters(self):
+        q, it, hs, ms = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_double()
+        L.check(self._lib.dat_get_counters(self._h, ctypes.byref(q), ctypes.byref(it), ctypes.byref(hs),
+                                           ctypes.byref(ms)))
+        return q.value, it.value, hs.value, ms.value
+
+    def reset_counters(self) -> None:
+        L.check(self._lib.dat_reset_counters(self._h))
+
+    def synchronize(self) -> None:
+        L.check(self._lib.dat_synchronize(self._h))
+
+
+# ================================================================================================
+# drop-in single-scenario controllers
+# ================================================================================================
+class _DropIn:
+    _mode = None
+
+    def __init__(self, params: RQPParameters, col: RQPCollision, state: RQPState, dt: float, env: Any = None,
+                 verbose: bool = False, device: int = 0) -> None:
+        assert params.n >= 3
+        self.n = params.n
+        self.params, self.col, self.dt, self.env, self.verbose = params, col, dt, env, verbose
+        self.max_f_ang = np.pi / 6.0
+        self.dist_eps = 0.1
+        self.vision_radius = col.collision_radius + 5.0
+        self._eng = BatchedController(self._mode, self.n, 1, pack_params(params, col), dt=dt, device=device,
+                                      record_err=self._mode != L.MODE_CENTRALIZED)
+        if env is not None:
+            self._eng.set_forests([env])
+
+    def control(self, state, acc_des):
+        acc = np.concatenate([np.asarray(acc_des[0], float), np.asarray(acc_des[1], float)])[None]
+        r = self._eng.control(pack_state(state)[None], acc)
+        f = r.f_des[0]
+        if self._mode == L.MODE_CENTRALIZED:
+            return f, SolverStatistics(-1, r.gpu_ms * 1e-3, bool(r.collision[0]), float(r.min_env_dist[0]))
+        it = int(r.iters[0])
+        err = r.err_seq[0][: max(it - 1, 0)].tolist() if r.err_seq is not None else []
+        err = [e for e in err if e == e]
+        return f, SolverStatistics(it, r.gpu_ms * 1e-3, bool(r.collision[0]), float(r.min_env_dist[0]), err)
+
+    def get_force_cone_angle_bound(self) -> float:
+        return self.max_f_ang
+
+    def get_dist_eps(self) -> float:
+        return self.dist_eps
+
+
+class RQPCentralizedController(_DropIn):
+    _mode = L.MODE_CENTRALIZED
+
+
+class RQPCADMMController(_DropIn):
+    _mode = L.MODE_CADMM
+
+    def set_force_err_tolerance(self, tol: float, use_total_res: bool = True) -> None:
+        self._eng.set_force_err_tolerance(tol, use_total_res)
+
+    def set_max_iter(self, max_iter: int) -> None:
+        self._eng.set_max_iter(max_iter)
+
+
+class RQPDDController(_DropIn):
+    _mode = L.MODE_DD
+
+    def set_force_err_tolerance(self, tol: float) -> None:
+        self._eng.set_force_err_tolerance(tol, True)
+
+    def set_max_iter(self, max_iter: int) -> None:
+        self._eng.set_max_iter(max_iter)
+
+
+class RQPClosedLoop:
+    """One scenario's closed loop on the GPU (example/rqp_example.py:120-131): HL control every
+    ``hl_rel_freq`` steps from the given desired accelerations, SO(3) PD low level and dynamics
+    at every step.  ``step(acc_des)`` advances one high-level period."""
+
+    def __init__(self, controller: _DropIn, state: RQPState, hl_rel_freq: int = 10) -> None:
+        self.ctrl = controller
+        self.hl = hl_rel_freq
+        self.ctrl._eng.set_state(pack_state(state)[None], np.zeros(1, dtype=np.int32))
+
+    def step(self, acc_des=None):
+        eng = self.ctrl._eng
+        acc = None
+        if acc_des is not None:
+            acc = np.concatenate([np.asarray(acc_des[0], float), np.asarray(acc_des[1], float)])[None]
+        r = eng.control(None, acc)
+        eng.rollout(self.hl)
+        return r
+
+    @property
+    def state(self) -> RQPState:
+        st, _ = self.ctrl._eng.get_state()
+        return RQPState.unpack(st[0], self.ctrl.n)
+
+
+__all__ = ["BatchedController", "StepResult", "SolverStatistics", "RQPCentralizedController", "RQPCADMMController",
+           "RQPDDController", "RQPClosedLoop"]

@@ -1,0 +1,1204 @@
+// dat.hip -- gfx950 kernels and the C-ABI (include/dat.h) of the batched agent-QP solver.
+//
+// Kernels (all fp64, no MFMA -- every contraction is <= 6 wide):
+//   k_cadmm    C-ADMM control step: one 64-lane wavefront holds floor(64/n) scenarios x n agents,
+//              one lane per agent QP; the whole ADMM loop (reference control/rqp_cadmm.py:631-675)
+//              runs on chip: agent QPs (ipm_solve), consensus mean / residual through LDS, dual
+//              update; per-scenario convergence masks.
+//   k_dd_setup DD quasi-Newton matrix H = A Q^-1 A' and its inverse per scenario, in LDS
+//              (control/rqp_dd.py:513-555, 634-657).
+//   k_dd       DD control step: prices, agent QPs, consensus error, dual ascent through H^-1
+//              (control/rqp_dd.py:659-752).
+//   k_cent     centralized QP, one lane per scenario (control/rqp_centralized.py:436-448).
+//   k_rollout  low-level SO(3) PD + dynamics + Lie integration, one lane per scenario.
+//   k_desired  forest desired-acceleration law (example/rqp_example.py:33-59).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dat.h"
+#include "dat_core.hpp"
+
+using namespace dat;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int NMAX = 16;        // largest team the kernels are compiled for
+constexpr int NMAX_DD = 8;      // DD master matrix is (6n)^2 in LDS
+constexpr int IPM_MAX_ITER = 50;
+constexpr double IPM_TOL = 1e-9;
+
+struct KArgs {
+  int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)
+  const double* params;
+  double* state;
+  int* counter;
+  const double* acc;
+  double* fdes;
+  const double* trees;
+  const int* tree_off;
+  const int* scen_forest;
+  int nforest;
+  const double* mountain;
+  int max_iter;
+  double res_tol;
+  int use_total_res;
+  double rho0, tau, rho_max;
+  int record_err;
+  double *cf, *cfbar, *clam;                 // C-ADMM warm state
+  double *dlamF, *dlamM, *dprev, *dHinv;      // DD state
+  double* pf;                                 // centralized previous solution
+  int* iters;
+  int* qstatus;
+  double* mind;
+  unsigned char* col;
+  double* err;
+  unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations
+};
+
+__device__ inline const double* prm_of(const KArgs& a, int sc) { return a.params + (a.ppp ? (size_t)sc * a.P : 0); }
+
+__device__ inline void forest_of(const KArgs& a, int sc, const double** trees, int* nt) {
+  *trees = nullptr;
+  *nt = 0;
+  if (a.nforest <= 0) return;
+  int f = a.scen_forest ? a.scen_forest[sc] : 0;
+  if (f < 0 || f >= a.nforest) return;
+  *trees = a.trees + 3 * (size_t)a.tree_off[f];
+  *nt = a.tree_off[f + 1] - a.tree_off[f];
+}
+
+// ------------------------------------------------------------------------------------------------
+// C-ADMM
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int n = a.n, N3 = 3 * n;
+  const int G = 64 / n, NT = G * n;
+  const int lane = threadIdx.x;
+  const int ls = lane / n, i = lane - ls * n;
+  const int sc = blockIdx.x * G + ls;
+  const bool valid = (lane < NT) && (sc < a.B);
+  double* fx = smem;                       // NT x 3n   agent copies f^(i)
+  double* fbar = fx + NT * N3;             // G x 3n    consensus mean
+  double* Rt = fbar + G * N3;              // G x 9n    hat(r_com_j) Rl'
+  double* red = Rt + G * 9 * n;            // 64 x 16   per-lane scratch
+  int* done = (int*)(red + 64 * 16);       // G
+  double* myf = fx + lane * N3;
+  double* fb = fbar + ls * N3;
+  double* rts = Rt + ls * 9 * n;
+  double* myred = red + lane * 16;
+
+  QP<1> P;
+  const double* prm = nullptr;
+  double* lam = nullptr;
+  int iter = 0, qstat = ST_OPTIMAL;
+  long long my_ipm = 0, my_qp = 0;
+  EnvOut env;
+  env.collision = 0;
+  env.min_env_dist = 0.0;
+  if (valid) {
+    prm = prm_of(a, sc);
+    const double* st = a.state + (size_t)sc * a.S;
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + 9 * i);
+    for (int c = 0; c < N3; ++c) myf[c] = a.cf[((size_t)sc * n + i) * N3 + c];
+    for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
+    lam = a.clam + ((size_t)sc * n + i) * N3;
+    if (i == 0) done[ls] = 0;
+  } else if (lane < NT && i == 0) {
+    done[ls] = 1;
+  }
+  __syncthreads();
+  if (valid) {
+    const double* st = a.state + (size_t)sc * a.S;
+    build_cadmm_static(P, prm, n, st, a.acc + (size_t)sc * 6, i, rts);
+    const double* trees;
+    int nt, nrow = 0;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &nrow, lhs, rhs);
+    add_env_rows(P, nrow, lhs, rhs);
+  }
+  double rho = a.rho0;
+  for (;;) {
+    const bool active = valid && !done[ls];
+    if (active) {
+      build_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
+      double y[1][3], w[6];
+      IPMOut o = ipm_solve<MODE_CADMM, 1>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+      my_ipm += o.iters;
+      ++my_qp;
+      qstat = o.status;
+      if (o.status == ST_OPTIMAL) {
+        double fnew[3 * NMAX];
+        cadmm_materialize(P, n, i, rts, lam, fb, y[0], o.pi, fnew);
+        for (int c = 0; c < N3; ++c) myf[c] = fnew[c];
+      } else if (o.status == ST_FAILED) {  // solver exception -> f_eq (control/rqp_cadmm.py:491-494)
+        for (int c = 0; c < N3; ++c) myf[c] = prm[DAT_P_FEQ(n) + c];
+      }  // otherwise hold the previous solution (control/rqp_cadmm.py:496-499)
+    }
+    __syncthreads();
+    if (active) {
+      ++iter;
+      rho = fmin(rho * a.tau, a.rho_max);
+      // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
+      for (int c = 0; c < 3; ++c) {
+        double s = 0.0;
+        for (int k = 0; k < n; ++k) s += fx[(ls * n + k) * N3 + 3 * i + c];
+        myred[8 + c] = s / n;
+      }
+    }
+    __syncthreads();
+    if (active) {
+      for (int c = 0; c < 3; ++c) fb[3 * i + c] = myred[8 + c];
+    }
+    __syncthreads();
+    if (active) {
+      if (a.use_total_res) {
+        double rmax = 0.0;
+        for (int r = 0; r < 3; ++r) {
+          double s = 0.0;
+          for (int j = 0; j < n; ++j) s += fabs(myf[3 * j + r] - fb[3 * j + r]);
+          rmax = fmax(rmax, s);
+        }
+        myred[0] = rmax;
+      } else {
+        // aggregate residual (control/rqp_cadmm.py:602-621)
+        double F[3] = {0, 0, 0}, M[3] = {0, 0, 0}, mi[3];
+        for (int j = 0; j < n; ++j) {
+          double m3[3];
+          mv3(rts + 9 * j, myf + 3 * j, m3);
+          if (j == i) {
+            mi[0] = m3[0]; mi[1] = m3[1]; mi[2] = m3[2];
+            continue;
+          }
+          for (int c = 0; c < 3; ++c) { F[c] += myf[3 * j + c]; M[c] += m3[c]; }
+        }
+        for (int c = 0; c < 3; ++c) {
+          myred[1 + c] = F[c];
+          myred[4 + c] = M[c];
+          myred[11 + c] = myf[3 * i + c];  // f_app
+        }
+        (void)mi;
+      }
+    }
+    __syncthreads();
+    if (active && !a.use_total_res) {
+      // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
+      double sf[3] = {0, 0, 0}, sm[3] = {0, 0, 0};
+      for (int k = 0; k < n; ++k) {
+        if (k == i) continue;
+        const double* fk = red + (ls * n + k) * 16 + 11;
+        double m3[3];
+        mv3(rts + 9 * k, fk, m3);
+        for (int c = 0; c < 3; ++c) { sf[c] += fk[c]; sm[c] += m3[c]; }
+      }
+      for (int c = 0; c < 3; ++c) {
+        myred[1 + c] -= sf[c];
+        myred[4 + c] -= sm[c];
+      }
+    }
+    __syncthreads();
+    if (active && i == 0) {
+      double res = 0.0;
+      if (a.use_total_res) {
+        for (int k = 0; k < n; ++k) res = fmax(res, red[(ls * n + k) * 16]);
+      } else {
+        for (int r = 0; r < 3; ++r) {
+          double sF = 0.0, sM = 0.0;
+          for (int k = 0; k < n; ++k) {
+            sF += fabs(red[(ls * n + k) * 16 + 1 + r]);
+            sM += fabs(red[(ls * n + k) * 16 + 4 + r]);
+          }
+          res = fmax(res, fmax(sF, sM));
+        }
+      }
+      bool stop = (res < a.res_tol) || (iter > a.max_iter);
+      if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
+      red[(ls * n) * 16 + 15] = stop ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (active) {
+      bool stop = red[(ls * n) * 16 + 15] != 0.0;
+      if (!stop) {
+        for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
+      }
+    }
+    __syncthreads();
+    int any = 0;
+    if (active && i == 0) {
+      bool stop = red[(ls * n) * 16 + 15] != 0.0;
+      done[ls] = stop ? 1 : 0;
+      any = stop ? 0 : 1;
+    }
+    if (!__syncthreads_or(any)) break;
+  }
+  // epilogue
+  if (valid) {
+    for (int c = 0; c < N3; ++c) a.cf[((size_t)sc * n + i) * N3 + c] = myf[c];
+    for (int c = 0; c < 3; ++c) {
+      a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
+      a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
+    }
+    a.qstatus[(size_t)sc * n + i] = qstat;
+    myred[0] = env.collision ? 1.0 : 0.0;
+    myred[1] = env.min_env_dist;
+  }
+  __syncthreads();
+  if (valid && i == 0) {
+    a.iters[sc] = iter;
+    int coll = 0;
+    double md = prm[DAT_P_VISR];
+    for (int k = 0; k < n; ++k) {
+      coll |= red[(ls * n + k) * 16] != 0.0;
+      md = fmin(md, red[(ls * n + k) * 16 + 1]);
+    }
+    a.col[sc] = (unsigned char)coll;
+    a.mind[sc] = md;
+  }
+  // work counters: one atomic per lane group
+  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm;
+  for (int off = 32; off > 0; off >>= 1) {
+    q += __shfl_xor(q, off);
+    ip += __shfl_xor(ip, off);
+  }
+  if (lane == 0) {
+    atomicAdd(a.counters, q);
+    atomicAdd(a.counters + 1, ip);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// DD: quasi-Newton matrix inverse per scenario (one 64-lane block per scenario)
+// ------------------------------------------------------------------------------------------------
+// Q_i: strong_convexity_matrix (control/rqp_dd.py:513-555), 9x9 in (f_i, F_i, M_i)
+__device__ void dd_strong_convexity(const double* prm, int n, const double* st, int i, double* Q) {
+  const double kf = prm[DAT_P_KFD], km = prm[DAT_P_KMD], kfeq = prm[DAT_P_KFEQ];
+  const double leader = (i == 0) ? 1.0 : 0.0;
+  const double mT = prm[DAT_P_MT];
+  const double* Rl = st + DAT_S_RL(n);
+  double Rt[9], Xh[9], RX[9], Bv[9];
+  make_Rt(prm + DAT_P_RCOM(n) + 3 * i, Rl, Rt);
+  skew3(prm + DAT_P_XCOM, Xh);
+  mm3(Rl, Xh, RX);
+  mm3(RX, prm + DAT_P_JTI, Bv);  // Rl hat(x_com) JT^-1
+  for (int k = 0; k < 81; ++k) Q[k] = 0.0;
+  for (int k = 0; k < 9; ++k) Q[10 * k] = 1e-6;
+  auto acc = [&](const double* T /*3x9*/, double wgt) {
+    for (int r = 0; r < 9; ++r)
+      for (int c = 0; c < 9; ++c) Q[9 * r + c] += 2.0 * wgt * (T[r] * T[c] + T[9 + r] * T[9 + c] + T[18 + r] * T[18 + c]);
+  };
+  double T[27];
+  for (int k = 0; k < 27; ++k) T[k] = 0.0;
+  for (int r = 0; r < 3; ++r) T[9 * r + r] = 1.0;          // [I 0 0]
+  acc(T, kfeq);
+  for (int r = 0; r < 3; ++r) T[9 * r + 3 + r] = 1.0;      // [I I 0]
+  acc(T, kf);
+  for (int k = 0; k < 27; ++k) T[k] = 0.0;                 // [Rt 0 I]
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) T[9 * r + c] = Rt[3 * r + c];
+    T[9 * r + 6 + r] = 1.0;
+  }
+  acc(T, km);
+  if (leader != 0.0) {
+    const double* JTi = prm + DAT_P_JTI;
+    double JR[9], BR[9];
+    mm3(JTi, Rt, JR);
+    mm3(Bv, Rt, BR);
+    for (int k = 0; k < 27; ++k) T[k] = 0.0;               // [JT^-1 Rt, 0, JT^-1]
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) { T[9 * r + c] = JR[3 * r + c]; T[9 * r + 6 + c] = JTi[3 * r + c]; }
+    acc(T, leader);
+    for (int k = 0; k < 27; ++k) T[k] = 0.0;               // [I/mT + Bv Rt, I/mT, Bv]
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        T[9 * r + c] = BR[3 * r + c] + (r == c ? 1.0 / mT : 0.0);
+        T[9 * r + 3 + c] = (r == c ? 1.0 / mT : 0.0);
+        T[9 * r + 6 + c] = Bv[3 * r + c];
+      }
+    acc(T, leader);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int n = a.n, N = 6 * n;
+  const int sc = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (sc >= a.B) return;
+  double* Qi = smem;              // n x 81   sym(Q_i^-1)
+  double* Rts = Qi + 81 * n;      // n x 9
+  double* H = Rts + 9 * n;        // N x 2N   [H | I]
+  double* fac = H + 2 * N * N;    // N
+  const double* prm = prm_of(a, sc);
+  const double* st = a.state + (size_t)sc * a.S;
+  if (lane < n) {
+    double Q[81], Aug[9][18];
+    dd_strong_convexity(prm, n, st, lane, Q);
+    for (int r = 0; r < 9; ++r)
+      for (int c = 0; c < 18; ++c) Aug[r][c] = c < 9 ? Q[9 * r + c] : (c - 9 == r ? 1.0 : 0.0);
+    for (int k = 0; k < 9; ++k) {  // Gauss-Jordan with partial pivoting (np.linalg.inv)
+      int p = k;
+      for (int r = k + 1; r < 9; ++r)
+        if (fabs(Aug[r][k]) > fabs(Aug[p][k])) p = r;
+      if (p != k)
+        for (int c = 0; c < 18; ++c) { double t = Aug[k][c]; Aug[k][c] = Aug[p][c]; Aug[p][c] = t; }
+      double inv = 1.0 / Aug[k][k];
+      for (int c = 0; c < 18; ++c) Aug[k][c] *= inv;
+      for (int r = 0; r < 9; ++r) {
+        if (r == k) continue;
+        double f = Aug[r][k];
+        for (int c = 0; c < 18; ++c) Aug[r][c] -= f * Aug[k][c];
+      }
+    }
+    for (int r = 0; r < 9; ++r)
+      for (int c = 0; c < 9; ++c) Qi[81 * lane + 9 * r + c] = 0.5 * (Aug[r][9 + c] + Aug[c][9 + r]);
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * lane, st + DAT_S_RL(n), Rts + 9 * lane);
+  }
+  __syncthreads();
+  // H = A blkdiag(Q_j^-1) A'  (control/rqp_dd.py:642-655); row r of A restricted to block j:
+  //   j == agent(r): unit vector e_{3 + comp};  j != agent(r): -e_comp (comp < 3) or -Rt_j[comp-3, :] on f_j
+  auto arow = [&](int r, int j, double* v) {
+    int ag = r / 6, comp = r % 6;
+    for (int k = 0; k < 9; ++k) v[k] = 0.0;
+    if (j == ag) {
+      v[3 + comp] = 1.0;
+    } else if (comp < 3) {
+      v[comp] = -1.0;
+    } else {
+      for (int k = 0; k < 3; ++k) v[k] = -Rts[9 * j + 3 * (comp - 3) + k];
+    }
+  };
+  for (int e = lane; e < N * N; e += 64) {
+    int r = e / N, c = e % N;
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) {
+      double vr[9], vc[9];
+      arow(r, j, vr);
+      arow(c, j, vc);
+      const double* Q = Qi + 81 * j;
+      for (int p = 0; p < 9; ++p) {
+        if (vr[p] == 0.0) continue;
+        double t = 0.0;
+        for (int q = 0; q < 9; ++q) t += Q[9 * p + q] * vc[q];
+        s += vr[p] * t;
+      }
+    }
+    H[2 * N * r + c] = s;
+    H[2 * N * r + N + c] = (r == c) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  // Gauss-Jordan on [H | I] (H is SPD: no pivoting needed)
+  for (int k = 0; k < N; ++k) {
+    double piv = H[2 * N * k + k];
+    __syncthreads();
+    for (int c = lane; c < 2 * N; c += 64) H[2 * N * k + c] /= piv;
+    __syncthreads();
+    for (int r = lane; r < N; r += 64) fac[r] = H[2 * N * r + k];
+    __syncthreads();
+    for (int e = lane; e < N * 2 * N; e += 64) {
+      int r = e / (2 * N), c = e % (2 * N);
+      if (r != k) H[2 * N * r + c] -= fac[r] * H[2 * N * k + c];
+    }
+    __syncthreads();
+  }
+  double* out = a.dHinv + (size_t)sc * N * N;
+  for (int e = lane; e < N * N; e += 64) out[e] = H[2 * N * (e / N) + N + (e % N)];
+}
+
+// ------------------------------------------------------------------------------------------------
+// DD step
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_dd(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int n = a.n, N3 = 3 * n, N6 = 6 * n;
+  const int G = 64 / n, NT = G * n;
+  const int lane = threadIdx.x;
+  const int ls = lane / n, i = lane - ls * n;
+  const int sc = blockIdx.x * G + ls;
+  const bool valid = (lane < NT) && (sc < a.B);
+  double* X = smem;                 // NT x 9   (f_i, F_i, M_i)
+  double* lamF = X + NT * 9;        // G x 3n
+  double* lamM = lamF + G * N3;     // G x 3n
+  double* E = lamM + G * N3;        // NT x 6   consensus error
+  double* Rts = E + NT * 6;         // G x 9n
+  double* red = Rts + G * 9 * n;    // 64 x 4
+  double* myX = X + lane * 9;
+  double* lF = lamF + ls * N3;
+  double* lM = lamM + ls * N3;
+  double* rts = Rts + ls * 9 * n;
+
+  QP<1> P;
+  const double* prm = nullptr;
+  double prev[9];
+  int iter = 0, qstat = ST_OPTIMAL;
+  long long my_ipm = 0, my_qp = 0;
+  EnvOut env;
+  env.collision = 0;
+  env.min_env_dist = 0.0;
+  if (valid) {
+    prm = prm_of(a, sc);
+    const double* st = a.state + (size_t)sc * a.S;
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + 9 * i);
+    for (int c = 0; c < 3; ++c) {
+      lF[3 * i + c] = a.dlamF[(size_t)sc * N3 + 3 * i + c];
+      lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
+    }
+    for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
+    build_dd_static(P, prm, n, st, a.acc + (size_t)sc * 6, i, rts + 9 * i);
+    const double* trees;
+    int nt, nrow = 0;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &nrow, lhs, rhs);
+    add_env_rows(P, nrow, lhs, rhs);
+  }
+  if (lane < 64) red[lane * 4 + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
+  __syncthreads();
+  const double* Rl = valid ? a.state + (size_t)sc * a.S + DAT_S_RL(n) : nullptr;
+  for (;;) {
+    const bool active = valid && red[(ls * n) * 4 + 3] == 0.0;
+    if (active) {
+      // prices (control/rqp_dd.py:718-722)
+      double sF[3] = {0, 0, 0}, sM[3] = {0, 0, 0};
+      for (int k = 0; k < n; ++k)
+        for (int c = 0; c < 3; ++c) { sF[c] += lF[3 * k + c]; sM[c] += lM[3 * k + c]; }
+      double c9[9], dm[3], rxd[3], Rr[3];
+      for (int c = 0; c < 3; ++c) dm[c] = sM[c] - lM[3 * i + c];
+      cross3(prm + DAT_P_RCOM(n) + 3 * i, dm, rxd);
+      mv3(Rl, rxd, Rr);
+      for (int c = 0; c < 3; ++c) {
+        c9[c] = -(sF[c] - lF[3 * i + c]) + Rr[c];
+        c9[3 + c] = lF[3 * i + c];
+        c9[6 + c] = lM[3 * i + c];
+      }
+      set_dd_price(P, prm, n, i, c9);
+      double y[1][3], w[6];
+      IPMOut o = ipm_solve<MODE_DD, 1>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+      my_ipm += o.iters;
+      ++my_qp;
+      qstat = o.status;
+      if (o.status == ST_OPTIMAL) {
+        for (int c = 0; c < 3; ++c) prev[c] = y[0][c];
+        for (int c = 0; c < 6; ++c) prev[3 + c] = w[c];
+      } else if (o.status == ST_FAILED) {  // control/rqp_dd.py:484-489
+        const double* feq = prm + DAT_P_FEQ(n);
+        double s3[3] = {0, 0, 0}, jr[3], rf[3];
+        for (int k = 0; k < n; ++k)
+          for (int c = 0; c < 3; ++c) s3[c] += feq[3 * k + c];
+        for (int c = 0; c < 3; ++c) { prev[c] = feq[3 * i + c]; prev[3 + c] = s3[c] - feq[3 * i + c]; }
+        cross3(prm + DAT_P_RCOM(n) + 3 * i, prev, rf);
+        mv3(prm + DAT_P_JTI, rf, jr);
+        for (int c = 0; c < 3; ++c) prev[6 + c] = -jr[c];
+      }
+      for (int c = 0; c < 9; ++c) myX[c] = prev[c];
+    }
+    __syncthreads();
+    if (active) {
+      ++iter;
+      // consensus error (control/rqp_dd.py:659-676)
+      double sf[3] = {0, 0, 0}, sm[3] = {0, 0, 0};
+      for (int k = 0; k < n; ++k) {
+        if (k == i) continue;
+        const double* fk = X + (ls * n + k) * 9;
+        double m3[3];
+        mv3(rts + 9 * k, fk, m3);
+        for (int c = 0; c < 3; ++c) { sf[c] += fk[c]; sm[c] += m3[c]; }
+      }
+      for (int c = 0; c < 3; ++c) {
+        E[lane * 6 + c] = myX[3 + c] - sf[c];
+        E[lane * 6 + 3 + c] = myX[6 + c] - sm[c];
+      }
+    }
+    __syncthreads();
+    if (active && i == 0) {
+      double res = 0.0;
+      for (int r = 0; r < 6; ++r) {
+        double s = 0.0;
+        for (int k = 0; k < n; ++k) s += fabs(E[(ls * n + k) * 6 + r]);
+        res = fmax(res, s);
+      }
+      bool stop = (res < a.res_tol) || (iter > a.max_iter);
+      if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
+      red[(ls * n) * 4 + 2] = stop ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (active && red[(ls * n) * 4 + 2] == 0.0) {
+      // dual ascent: lambda += H^-1 (A x)   (control/rqp_dd.py:678-693); rows 6i..6i+5
+      const double* Hi = a.dHinv + (size_t)sc * N6 * N6;
+      double stp[6];
+      for (int r = 0; r < 6; ++r) {
+        const double* row = Hi + (size_t)(6 * i + r) * N6;
+        double s = 0.0;
+        for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * 6 + c % 6];
+        stp[r] = s;
+      }
+      red[lane * 4 + 0] = 0.0;
+      for (int c = 0; c < 3; ++c) {
+        lF[3 * i + c] += stp[c];
+        lM[3 * i + c] += stp[3 + c];
+      }
+    }
+    __syncthreads();
+    int any = 0;
+    if (active && i == 0) {
+      bool stop = red[(ls * n) * 4 + 2] != 0.0;
+      red[(ls * n) * 4 + 3] = stop ? 1.0 : 0.0;
+      any = stop ? 0 : 1;
+    }
+    if (!__syncthreads_or(any)) break;
+  }
+  if (valid) {
+    for (int c = 0; c < 3; ++c) {
+      a.dlamF[(size_t)sc * N3 + 3 * i + c] = lF[3 * i + c];
+      a.dlamM[(size_t)sc * N3 + 3 * i + c] = lM[3 * i + c];
+      a.fdes[(size_t)sc * N3 + 3 * i + c] = myX[c];
+    }
+    for (int c = 0; c < 9; ++c) a.dprev[((size_t)sc * n + i) * 9 + c] = prev[c];
+    a.qstatus[(size_t)sc * n + i] = qstat;
+    red[lane * 4 + 0] = env.collision ? 1.0 : 0.0;
+    red[lane * 4 + 1] = env.min_env_dist;
+  }
+  __syncthreads();
+  if (valid && i == 0) {
+    a.iters[sc] = iter;
+    int coll = 0;
+    double md = prm[DAT_P_VISR];
+    for (int k = 0; k < n; ++k) {
+      coll |= red[(ls * n + k) * 4] != 0.0;
+      md = fmin(md, red[(ls * n + k) * 4 + 1]);
+    }
+    a.col[sc] = (unsigned char)coll;
+    a.mind[sc] = md;
+  }
+  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm;
+  for (int off = 32; off > 0; off >>= 1) {
+    q += __shfl_xor(q, off);
+    ip += __shfl_xor(ip, off);
+  }
+  if (lane == 0) {
+    atomicAdd(a.counters, q);
+    atomicAdd(a.counters + 1, ip);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// centralized: one lane per scenario
+// ------------------------------------------------------------------------------------------------
+template <int NB>
+__global__ __launch_bounds__(64) void k_cent(KArgs a) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long q = 0, ip = 0;
+  if (sc < a.B) {
+    const int n = NB;
+    const double* prm = prm_of(a, sc);
+    const double* st = a.state + (size_t)sc * a.S;
+    QP<NB> P;
+    build_cent<NB>(P, prm, n, st, a.acc + (size_t)sc * 6);
+    const double* trees;
+    int nt, nrow = 0;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    EnvOut env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &nrow, lhs, rhs);
+    add_env_rows(P, nrow, lhs, rhs);
+    double y[NB][3], w[6];
+    IPMOut o = ipm_solve<MODE_CENT, NB>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+    q = 1;
+    ip = o.iters;
+    double* pf = a.pf + (size_t)sc * 3 * n;
+    if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
+      for (int k = 0; k < NB; ++k)
+        for (int c = 0; c < 3; ++c) pf[3 * k + c] = y[k][c];
+    for (int c = 0; c < 3 * n; ++c) a.fdes[(size_t)sc * 3 * n + c] = pf[c];
+    for (int k = 0; k < n; ++k) a.qstatus[(size_t)sc * n + k] = o.status;
+    a.iters[sc] = -1;
+    a.col[sc] = (unsigned char)env.collision;
+    a.mind[sc] = env.min_env_dist;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    q += __shfl_xor(q, off);
+    ip += __shfl_xor(ip, off);
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(a.counters, q);
+    atomicAdd(a.counters + 1, ip);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// rollout / desired acceleration / warm start
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_rollout(KArgs a, int steps, double dt, const double* fdes) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc >= a.B) return;
+  const int n = a.n;
+  const double* prm = prm_of(a, sc);
+  double st[DAT_STATE_SIZE(NMAX)];
+  double* g = a.state + (size_t)sc * a.S;
+  for (int k = 0; k < a.S; ++k) st[k] = g[k];
+  int cnt = a.counter[sc];
+  const double* fd = fdes + (size_t)sc * 3 * n;
+  for (int s = 0; s < steps; ++s) sim_step<NMAX>(prm, n, st, &cnt, fd, dt);
+  for (int k = 0; k < a.S; ++k) g[k] = st[k];
+  a.counter[sc] = cnt;
+}
+
+__global__ void k_desired(KArgs a, double* acc) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc >= a.B) return;
+  const double* st = a.state + (size_t)sc * a.S;
+  double* o = acc + (size_t)sc * 6;
+  int f = (a.nforest > 0) ? (a.scen_forest ? a.scen_forest[sc] : 0) : -1;
+  if (f < 0 || a.mountain == nullptr) {
+    double m0[DAT_MOUNTAIN_SIZE] = {30.0, 0.0, 25.0, 1e300, 0.0};
+    desired_accel_forest(st, a.n, m0, 1.5, o);
+  } else {
+    desired_accel_forest(st, a.n, a.mountain + (size_t)f * DAT_MOUNTAIN_SIZE, 1.5, o);
+  }
+}
+
+__global__ void k_warm(KArgs a) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc >= a.B) return;
+  const int n = a.n, N3 = 3 * n;
+  const double* prm = prm_of(a, sc);
+  const double* feq = prm + DAT_P_FEQ(n);
+  if (a.cf) {
+    for (int i = 0; i < n; ++i)
+      for (int c = 0; c < N3; ++c) {
+        a.cf[((size_t)sc * n + i) * N3 + c] = feq[c];
+        a.clam[((size_t)sc * n + i) * N3 + c] = 0.0;
+      }
+    for (int c = 0; c < N3; ++c) a.cfbar[(size_t)sc * N3 + c] = feq[c];
+  }
+  if (a.dlamF) {
+    double s3[3] = {0, 0, 0};
+    for (int k = 0; k < n; ++k)
+      for (int c = 0; c < 3; ++c) s3[c] += feq[3 * k + c];
+    for (int c = 0; c < N3; ++c) { a.dlamF[(size_t)sc * N3 + c] = 0.0; a.dlamM[(size_t)sc * N3 + c] = 0.0; }
+    for (int i = 0; i < n; ++i) {
+      double* pv = a.dprev + ((size_t)sc * n + i) * 9;
+      for (int c = 0; c < 3; ++c) { pv[c] = feq[3 * i + c]; pv[3 + c] = s3[c] - feq[3 * i + c]; }
+      double rf[3], jr[3];
+      cross3(prm + DAT_P_RCOM(n) + 3 * i, pv, rf);
+      mv3(prm + DAT_P_JTI, rf, jr);
+      for (int c = 0; c < 3; ++c) pv[6 + c] = -jr[c];
+    }
+  }
+  if (a.pf)
+    for (int c = 0; c < N3; ++c) a.pf[(size_t)sc * N3 + c] = feq[c];
+  for (int c = 0; c < N3; ++c) a.fdes[(size_t)sc * N3 + c] = feq[c];
+}
+
+__global__ void k_env(KArgs a, double* lhs, double* rhs, int* nrow, unsigned char* col, double* md) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.n;
+  if (t >= a.B * n) return;
+  const int sc = t / n, i = t % n;
+  const double* prm = prm_of(a, sc);
+  const double* st = a.state + (size_t)sc * a.S;
+  const double* trees;
+  int nt, k = 0;
+  forest_of(a, sc, &trees, &nt);
+  double L[DAT_NENV][3], R[DAT_NENV];
+  bool cent = (a.cf == nullptr && a.dlamF == nullptr);
+  EnvOut e = env_rows(prm, n, st, trees, nt, cent ? -1 : i, cent ? prm[DAT_P_AENVC] : prm[DAT_P_AENVD], &k, L, R);
+  for (int r = 0; r < DAT_NENV; ++r) {
+    for (int c = 0; c < 3; ++c) lhs[((size_t)t * DAT_NENV + r) * 3 + c] = r < k ? L[r][c] : 0.0;
+    rhs[(size_t)t * DAT_NENV + r] = r < k ? R[r] : 0.0;
+  }
+  nrow[t] = k;
+  col[t] = (unsigned char)e.collision;
+  md[t] = e.min_env_dist;
+}
+
+}  // namespace
+
+// ================================================================================================
+// handle + C-ABI
+// ================================================================================================
+struct dat_handle {
+  dat_config cfg;
+  int P = 0, S = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  double* params = nullptr;
+  int ppp = 0;
+  bool have_params = false;
+  double *state = nullptr, *acc = nullptr, *fdes = nullptr;
+  int* counter = nullptr;
+  double* trees = nullptr;
+  int* tree_off = nullptr;
+  int* scen_forest = nullptr;
+  double* mountain = nullptr;
+  int nforest = 0;
+  double *cf = nullptr, *cfbar = nullptr, *clam = nullptr;
+  double *dlamF = nullptr, *dlamM = nullptr, *dprev = nullptr, *dHinv = nullptr;
+  double* pf = nullptr;
+  int *iters = nullptr, *qstatus = nullptr;
+  double *mind = nullptr, *err = nullptr;
+  unsigned char* col = nullptr;
+  unsigned long long* counters = nullptr;
+  long long hl_steps = 0;
+  double hl_ms = 0.0;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(dat_handle* h, T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) return 0;
+  HIPCHK(hipMalloc((void**)p, count * sizeof(T)));
+  HIPCHK(hipMemsetAsync(*p, 0, count * sizeof(T), h->stream));
+  h->allocs.push_back(*p);
+  return 0;
+}
+
+void dfree(dat_handle* h, void* p) {
+  if (!p) return;
+  for (auto& q : h->allocs)
+    if (q == p) q = nullptr;
+  (void)hipFree(p);
+}
+
+KArgs kargs(dat_handle* h) {
+  KArgs a;
+  memset(&a, 0, sizeof(a));
+  const dat_config& c = h->cfg;
+  a.B = c.batch;
+  a.n = c.n;
+  a.P = h->P;
+  a.S = h->S;
+  a.ppp = h->ppp;
+  a.params = h->params;
+  a.state = h->state;
+  a.counter = h->counter;
+  a.acc = h->acc;
+  a.fdes = h->fdes;
+  a.trees = h->trees;
+  a.tree_off = h->tree_off;
+  a.scen_forest = h->scen_forest;
+  a.nforest = h->nforest;
+  a.mountain = h->mountain;
+  a.max_iter = c.max_iter;
+  a.res_tol = c.res_tol;
+  a.use_total_res = c.use_total_res;
+  a.rho0 = c.rho0;
+  a.tau = c.tau_incr;
+  a.rho_max = c.rho_max;
+  a.record_err = c.record_err;
+  a.cf = h->cf;
+  a.cfbar = h->cfbar;
+  a.clam = h->clam;
+  a.dlamF = h->dlamF;
+  a.dlamM = h->dlamM;
+  a.dprev = h->dprev;
+  a.dHinv = h->dHinv;
+  a.pf = h->pf;
+  a.iters = h->iters;
+  a.qstatus = h->qstatus;
+  a.mind = h->mind;
+  a.col = h->col;
+  a.err = h->err;
+  a.counters = h->counters;
+  return a;
+}
+
+size_t cadmm_lds(int n) {
+  int G = 64 / n, NT = G * n;
+  return sizeof(double) * ((size_t)NT * 3 * n + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * 16) + sizeof(int) * 64;
+}
+size_t dd_lds(int n) {
+  int G = 64 / n, NT = G * n;
+  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * 6 + (size_t)G * 9 * n + 64 * 4);
+}
+size_t dd_setup_lds(int n) {
+  int N = 6 * n;
+  return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + 2 * (size_t)N * N + N);
+}
+
+int launch_hl(dat_handle* h) {
+  KArgs a = kargs(h);
+  const int n = h->cfg.n, B = h->cfg.batch;
+  if (!h->have_params) return fail("dat_set_params has not been called");
+  if (h->cfg.record_err && h->err)
+    HIPCHK(hipMemsetAsync(h->err, 0xff, sizeof(double) * (size_t)B * (h->cfg.max_iter + 1), h->stream));  // NaN pad
+  HIPCHK(hipEventRecord(h->e0, h->stream));
+  if (h->cfg.mode == DAT_MODE_CADMM) {
+    int G = 64 / n;
+    int blocks = (B + G - 1) / G;
+    hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds(n), h->stream, a);
+  } else if (h->cfg.mode == DAT_MODE_DD) {
+    hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
+    int G = 64 / n;
+    int blocks = (B + G - 1) / G;
+    hipLaunchKernelGGL(k_dd, dim3(blocks), dim3(64), dd_lds(n), h->stream, a);
+  } else {
+    int blocks = (B + 63) / 64;
+    if (n == 3)
+      hipLaunchKernelGGL(k_cent<3>, dim3(blocks), dim3(64), 0, h->stream, a);
+    else
+      hipLaunchKernelGGL(k_cent<6>, dim3(blocks), dim3(64), 0, h->stream, a);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(h->e1, h->stream));
+  return 0;
+}
+
+int finish_hl(dat_handle* h) {
+  HIPCHK(hipEventSynchronize(h->e1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, h->e0, h->e1));
+  h->hl_ms += ms;
+  h->hl_steps += 1;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void dat_default_config(dat_config* c) {
+  memset(c, 0, sizeof(*c));
+  c->device = 0;
+  c->mode = DAT_MODE_CADMM;
+  c->n = 3;
+  c->batch = 1;
+  c->dt = 1e-3;
+  c->hl_every = 10;
+  c->max_iter = 100;
+  c->res_tol = 1e-2;
+  c->use_total_res = 1;
+  c->rho0 = 1.0;
+  c->tau_incr = 1.0;
+  c->rho_max = 2.0;
+  c->record_err = 0;
+}
+
+const char* dat_last_error(void) { return g_err.c_str(); }
+
+int dat_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int dat_create(const dat_config* cfg, dat_handle** out) {
+  if (!cfg || !out) return fail("dat_create: null argument");
+  *out = nullptr;
+  const dat_config& c = *cfg;
+  if (c.n < 3 || c.n > NMAX) return fail("dat_create: n must be in [3, 16]");
+  if (c.mode == DAT_MODE_DD && c.n > NMAX_DD) return fail("dat_create: DD supports n <= 8");
+  if (c.mode == DAT_MODE_CENTRALIZED && c.n != 3 && c.n != 6) return fail("dat_create: centralized supports n in {3, 6}");
+  if (c.mode < 0 || c.mode > 2) return fail("dat_create: bad mode");
+  if (c.batch < 1) return fail("dat_create: batch must be >= 1");
+  if (c.max_iter < 0) return fail("dat_create: max_iter must be >= 0");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (c.device < 0 || c.device >= ndev) return fail("dat_create: no such HIP device");
+  HIPCHK(hipSetDevice(c.device));
+  dat_handle* h = new dat_handle();
+  h->cfg = c;
+  h->P = DAT_PARAM_SIZE(c.n);
+  h->S = DAT_STATE_SIZE(c.n);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&h->e0) != hipSuccess || hipEventCreate(&h->e1) != hipSuccess) {
+    delete h;
+    return fail("dat_create: stream/event creation failed");
+  }
+  const size_t B = c.batch, n = c.n, N3 = 3 * n;
+  int rc = 0;
+  rc |= dalloc(h, &h->state, B * h->S);
+  rc |= dalloc(h, &h->counter, B);
+  rc |= dalloc(h, &h->acc, B * 6);
+  rc |= dalloc(h, &h->fdes, B * N3);
+  rc |= dalloc(h, &h->iters, B);
+  rc |= dalloc(h, &h->qstatus, B * n);
+  rc |= dalloc(h, &h->mind, B);
+  rc |= dalloc(h, &h->col, B);
+  rc |= dalloc(h, &h->counters, 2);
+  if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
+  if (c.mode == DAT_MODE_CADMM) {
+    rc |= dalloc(h, &h->cf, B * n * N3);
+    rc |= dalloc(h, &h->cfbar, B * N3);
+    rc |= dalloc(h, &h->clam, B * n * N3);
+  } else if (c.mode == DAT_MODE_DD) {
+    rc |= dalloc(h, &h->dlamF, B * N3);
+    rc |= dalloc(h, &h->dlamM, B * N3);
+    rc |= dalloc(h, &h->dprev, B * n * 9);
+    rc |= dalloc(h, &h->dHinv, B * 36 * n * n);
+  } else {
+    rc |= dalloc(h, &h->pf, B * N3);
+  }
+  if (rc) {
+    std::string m = g_err;
+    dat_destroy(h);
+    return fail(m);
+  }
+  // LDS budgets
+  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
+  if (lds > 160 * 1024) {
+    dat_destroy(h);
+    return fail("dat_create: LDS budget exceeded");
+  }
+  *out = h;
+  return 0;
+}
+
+int dat_destroy(dat_handle* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->cfg.device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void* p : h->allocs)
+    if (p) (void)hipFree(p);
+  if (h->e0) (void)hipEventDestroy(h->e0);
+  if (h->e1) (void)hipEventDestroy(h->e1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int dat_set_params(dat_handle* h, const double* params, int per_scenario) {
+  if (!h || !params) return fail("dat_set_params: null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  size_t count = (per_scenario ? (size_t)h->cfg.batch : 1) * h->P;
+  if (h->params) dfree(h, h->params);
+  if (dalloc(h, &h->params, count)) return -1;
+  HIPCHK(hipMemcpyAsync(h->params, params, count * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  h->ppp = per_scenario ? 1 : 0;
+  h->have_params = true;
+  return dat_reset_warm_start(h);
+}
+
+int dat_set_forests(dat_handle* h, int num_forests, const int* tree_offsets, const double* tree_pos,
+                    const int* scenario_forest, const double* mountain) {
+  if (!h) return fail("dat_set_forests: null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  dfree(h, h->trees);
+  dfree(h, h->tree_off);
+  dfree(h, h->scen_forest);
+  dfree(h, h->mountain);
+  h->trees = nullptr;
+  h->tree_off = nullptr;
+  h->scen_forest = nullptr;
+  h->mountain = nullptr;
+  h->nforest = 0;
+  if (num_forests <= 0) return 0;
+  if (!tree_offsets || !tree_pos) return fail("dat_set_forests: null forest data");
+  const int T = tree_offsets[num_forests];
+  if (T < 0) return fail("dat_set_forests: bad offsets");
+  for (int f = 0; f < num_forests; ++f)
+    if (tree_offsets[f + 1] < tree_offsets[f]) return fail("dat_set_forests: offsets must be non-decreasing");
+  if (dalloc(h, &h->trees, (size_t)(T > 0 ? T : 1) * 3) || dalloc(h, &h->tree_off, num_forests + 1)) return -1;
+  if (T > 0) HIPCHK(hipMemcpyAsync(h->trees, tree_pos, sizeof(double) * 3 * T, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->tree_off, tree_offsets, sizeof(int) * (num_forests + 1), hipMemcpyHostToDevice, h->stream));
+  if (scenario_forest) {
+    for (int s = 0; s < h->cfg.batch; ++s)
+      if (scenario_forest[s] >= num_forests) return fail("dat_set_forests: scenario_forest out of range");
+    if (dalloc(h, &h->scen_forest, h->cfg.batch)) return -1;
+    HIPCHK(hipMemcpyAsync(h->scen_forest, scenario_forest, sizeof(int) * h->cfg.batch, hipMemcpyHostToDevice, h->stream));
+  }
+  if (mountain) {
+    if (dalloc(h, &h->mountain, (size_t)num_forests * DAT_MOUNTAIN_SIZE)) return -1;
+    HIPCHK(hipMemcpyAsync(h->mountain, mountain, sizeof(double) * num_forests * DAT_MOUNTAIN_SIZE, hipMemcpyHostToDevice,
+                          h->stream));
+  }
+  h->nforest = num_forests;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res) {
+  if (!h) return fail("null handle");
+  h->cfg.res_tol = res_tol;
+  h->cfg.use_total_res = use_total_res;
+  return 0;
+}
+
+int dat_set_max_iter(dat_handle* h, int max_iter) {
+  if (!h) return fail("null handle");
+  if (max_iter < 0) return fail("dat_set_max_iter: negative");
+  if (h->cfg.record_err && max_iter > h->cfg.max_iter) {
+    HIPCHK(hipSetDevice(h->cfg.device));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    dfree(h, h->err);
+    h->err = nullptr;
+    if (dalloc(h, &h->err, (size_t)h->cfg.batch * (max_iter + 1))) return -1;
+  }
+  h->cfg.max_iter = max_iter;
+  return 0;
+}
+
+int dat_reset_warm_start(dat_handle* h) {
+  if (!h) return fail("null handle");
+  if (!h->have_params) return fail("dat_reset_warm_start: params not set");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  KArgs a = kargs(h);
+  hipLaunchKernelGGL(k_warm, dim3((h->cfg.batch + 63) / 64), dim3(64), 0, h->stream, a);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_set_state(dat_handle* h, const double* state, const int* counters) {
+  if (!h || !state) return fail("dat_set_state: null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipMemcpyAsync(h->state, state, sizeof(double) * (size_t)h->cfg.batch * h->S, hipMemcpyHostToDevice, h->stream));
+  if (counters)
+    HIPCHK(hipMemcpyAsync(h->counter, counters, sizeof(int) * h->cfg.batch, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_get_state(dat_handle* h, double* state, int* counters) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  if (state)
+    HIPCHK(hipMemcpyAsync(state, h->state, sizeof(double) * (size_t)h->cfg.batch * h->S, hipMemcpyDeviceToHost, h->stream));
+  if (counters)
+    HIPCHK(hipMemcpyAsync(counters, h->counter, sizeof(int) * h->cfg.batch, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_control_step(dat_handle* h, const double* state, const double* acc_des, double* f_des, int* iters,
+                     int* qp_status, double* min_env_dist, unsigned char* collision, double* err_seq) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n;
+  if (state) HIPCHK(hipMemcpyAsync(h->state, state, sizeof(double) * B * h->S, hipMemcpyHostToDevice, h->stream));
+  KArgs a = kargs(h);
+  if (acc_des) {
+    HIPCHK(hipMemcpyAsync(h->acc, acc_des, sizeof(double) * B * 6, hipMemcpyHostToDevice, h->stream));
+  } else {
+    hipLaunchKernelGGL(k_desired, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->acc);
+    HIPCHK(hipGetLastError());
+  }
+  if (launch_hl(h)) return -1;
+  if (f_des) HIPCHK(hipMemcpyAsync(f_des, h->fdes, sizeof(double) * B * 3 * n, hipMemcpyDeviceToHost, h->stream));
+  if (iters) HIPCHK(hipMemcpyAsync(iters, h->iters, sizeof(int) * B, hipMemcpyDeviceToHost, h->stream));
+  if (qp_status) HIPCHK(hipMemcpyAsync(qp_status, h->qstatus, sizeof(int) * B * n, hipMemcpyDeviceToHost, h->stream));
+  if (min_env_dist) HIPCHK(hipMemcpyAsync(min_env_dist, h->mind, sizeof(double) * B, hipMemcpyDeviceToHost, h->stream));
+  if (collision) HIPCHK(hipMemcpyAsync(collision, h->col, B, hipMemcpyDeviceToHost, h->stream));
+  if (err_seq) {
+    if (!h->err) return fail("dat_control_step: err_seq requested but record_err = 0");
+    HIPCHK(hipMemcpyAsync(err_seq, h->err, sizeof(double) * B * (h->cfg.max_iter + 1), hipMemcpyDeviceToHost, h->stream));
+  }
+  if (finish_hl(h)) return -1;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_rollout(dat_handle* h, int steps, const double* f_des) {
+  if (!h) return fail("null handle");
+  if (steps <= 0) return 0;
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n;
+  if (f_des) HIPCHK(hipMemcpyAsync(h->fdes, f_des, sizeof(double) * B * 3 * n, hipMemcpyHostToDevice, h->stream));
+  if (!h->have_params) return fail("dat_rollout: params not set");
+  KArgs a = kargs(h);
+  hipLaunchKernelGGL(k_rollout, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, steps, h->cfg.dt, (const double*)h->fdes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_closed_loop(dat_handle* h, int hl_steps) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch;
+  KArgs a = kargs(h);
+  for (int s = 0; s < hl_steps; ++s) {
+    hipLaunchKernelGGL(k_desired, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->acc);
+    if (launch_hl(h)) return -1;
+    hipLaunchKernelGGL(k_rollout, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->cfg.hl_every, h->cfg.dt,
+                       (const double*)h->fdes);
+    HIPCHK(hipGetLastError());
+    if (finish_hl(h)) return -1;
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* hl_steps, double* hl_kernel_ms) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (qp_solves) *qp_solves = (long long)c[0];
+  if (ipm_iters) *ipm_iters = (long long)c[1];
+  if (hl_steps) *hl_steps = h->hl_steps;
+  if (hl_kernel_ms) *hl_kernel_ms = h->hl_ms;
+  return 0;
+}
+
+int dat_reset_counters(dat_handle* h) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipMemsetAsync(h->counters, 0, 2 * sizeof(unsigned long long), h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->hl_steps = 0;
+  h->hl_ms = 0.0;
+  return 0;
+}
+
+int dat_synchronize(dat_handle* h) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_env_rows(dat_handle* h, double* lhs, double* rhs, int* nrow, unsigned char* collision, double* min_dist) {
+  if (!h || !lhs || !rhs || !nrow || !collision || !min_dist) return fail("dat_env_rows: null argument");
+  if (!h->have_params) return fail("dat_env_rows: params not set");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n, T = B * n;
+  double *dl, *dr, *dm;
+  int* dn;
+  unsigned char* dc;
+  HIPCHK(hipMalloc(&dl, sizeof(double) * T * DAT_NENV * 3));
+  HIPCHK(hipMalloc(&dr, sizeof(double) * T * DAT_NENV));
+  HIPCHK(hipMalloc(&dm, sizeof(double) * T));
+  HIPCHK(hipMalloc(&dn, sizeof(int) * T));
+  HIPCHK(hipMalloc(&dc, T));
+  KArgs a = kargs(h);
+  hipLaunchKernelGGL(k_env, dim3((T + 63) / 64), dim3(64), 0, h->stream, a, dl, dr, dn, dc, dm);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(lhs, dl, sizeof(double) * T * DAT_NENV * 3, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(rhs, dr, sizeof(double) * T * DAT_NENV, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(nrow, dn, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(collision, dc, T, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(min_dist, dm, sizeof(double) * T, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(dl);
+  (void)hipFree(dr);
+  (void)hipFree(dm);
+  (void)hipFree(dn);
+  (void)hipFree(dc);
+  if (e != hipSuccess) return fail(std::string("dat_env_rows: ") + hipGetErrorString(e));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+/* dat.h -- C-ABI of the MI355X batched agent-QP solver (libdat.so).
+ *
+ * Drop-in boundary for the reference's controller hot path.  In the reference
+ * (AkshayThiru/distributed-aerial-transportation) the plug-in point is the cvxpy solver
+ * backend: control/rqp_cadmm.py:16-17 (_RQPCDMM_SOLVER = cv.CLARABEL), control/rqp_dd.py:17-18
+ * (_RQPDD_SOLVER) and control/rqp_centralized.py:132,440 (cv.CLARABEL literal), called once per
+ * agent QP from RQPPrimalSolver.solve (control/rqp_cadmm.py:482-501, control/rqp_dd.py:475-505)
+ * and RQPCentralizedController.control (control/rqp_centralized.py:436-448).  This library
+ * replaces that per-call path with batched calls over B independent scenarios; the Python
+ * controller classes in distributed_aerial_transportation_amd/control.py keep the reference
+ * constructor and control(state, acc_des) signatures on top of it.
+ *
+ * Conventions: fp64 everywhere; caller-owned, C-contiguous host buffers, read/written only
+ * during the call; block layouts in distributed_aerial_transportation_amd/csrc/dat_layout.h;
+ * return 0 on success, < 0 on error (message via dat_last_error()); no C++ exceptions cross
+ * the ABI.  A handle is bound to one HIP device and one stream and is not re-entrant.
+ */
+#ifndef DAT_H
+#define DAT_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAT_MODE_CENTRALIZED 0 /* RQPCentralizedController  control/rqp_centralized.py:27-455 */
+#define DAT_MODE_CADMM 1       /* RQPCADMMController         control/rqp_cadmm.py:510-688    */
+#define DAT_MODE_DD 2          /* RQPDDController            control/rqp_dd.py:558-764       */
+
+/* per agent-QP status (maps the cvxpy/Clarabel outcomes the reference branches on) */
+#define DAT_QP_OPTIMAL 0    /* accepted                         (prob.status == OPTIMAL)        */
+#define DAT_QP_INACCURATE 1 /* previous solution held           (non-OPTIMAL status)            */
+#define DAT_QP_INFEASIBLE 2 /* previous solution held           (non-OPTIMAL status)            */
+#define DAT_QP_FAILED 3     /* equilibrium forces used          (solver exception, :491-494)    */
+
+typedef struct dat_handle dat_handle;
+
+typedef struct dat_config {
+  int device;        /* HIP device ordinal                                               */
+  int mode;          /* DAT_MODE_*                                                       */
+  int n;             /* quadrotors per payload (3 <= n <= 16; DD n <= 8; centralized 3|6) */
+  int batch;         /* number of independent scenarios B                                */
+  double dt;         /* simulation step [s] (example/rqp_example.py:85: 1e-3)            */
+  int hl_every;      /* simulation steps per high-level step (rqp_example.py:86: 10)     */
+  int max_iter;      /* ADMM/DD max_iter (control/rqp_cadmm.py:563: 100)                 */
+  double res_tol;    /* ADMM/DD residual tolerance (control/rqp_cadmm.py:561: 1e-2)      */
+  int use_total_res; /* C-ADMM residual kind (control/rqp_cadmm.py:562: 1)               */
+  double rho0, tau_incr, rho_max; /* C-ADMM penalty schedule (control/rqp_cadmm.py:565-567) */
+  int record_err;    /* keep per-iteration residual sequences (SolverStatistics.err_seq) */
+} dat_config;
+
+/* ---- lifecycle ------------------------------------------------------------------------- */
+void dat_default_config(dat_config* cfg);
+int dat_create(const dat_config* cfg, dat_handle** out);
+int dat_destroy(dat_handle* h);
+const char* dat_last_error(void); /* thread-local message of the last failing call */
+int dat_device_count(void);
+
+/* ---- problem data ------------------------------------------------------------------------ */
+/* params: per_scenario ? B x DAT_PARAM_SIZE(n) : DAT_PARAM_SIZE(n) (broadcast) */
+int dat_set_params(dat_handle* h, const double* params, int per_scenario);
+/* forests: num_forests layouts; tree_offsets[num_forests+1] index rows of tree_pos (T x 3);
+ * scenario_forest[B] selects a layout per scenario (NULL: all use layout 0, -1: no env);
+ * mountain[num_forests x DAT_MOUNTAIN_SIZE] for the desired-acceleration law.  num_forests = 0
+ * removes the environment (env = None in the reference). */
+int dat_set_forests(dat_handle* h, int num_forests, const int* tree_offsets, const double* tree_pos,
+                    const int* scenario_forest, const double* mountain);
+int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res); /* set_force_err_tolerance */
+int dat_set_max_iter(dat_handle* h, int max_iter);                       /* set_max_iter           */
+int dat_reset_warm_start(dat_handle* h); /* controller construction state (f = f_eq, lambda = 0) */
+
+/* ---- state ------------------------------------------------------------------------------ */
+int dat_set_state(dat_handle* h, const double* state /* B x DAT_STATE_SIZE(n) */, const int* counters /* B or NULL */);
+int dat_get_state(dat_handle* h, double* state, int* counters);
+
+/* ---- one high-level control step for every scenario ---------------------------------------
+ * state: B x DAT_STATE_SIZE(n) or NULL (use the device-resident state);
+ * acc_des: B x 6 (dvl_des, dwl_des) or NULL (forest law example/rqp_example.py:33-59 on device).
+ * Outputs (any may be NULL): f_des B x 3n (agent-major, the forces the controller returns),
+ * iters B (SolverStatistics.iter; -1 for centralized), qp_status B x n (last solve per agent),
+ * min_env_dist B, collision B, err_seq B x (max_iter+1) (NaN padded; needs record_err). */
+int dat_control_step(dat_handle* h, const double* state, const double* acc_des, double* f_des, int* iters,
+                     int* qp_status, double* min_env_dist, unsigned char* collision, double* err_seq);
+
+/* ---- rollout: `steps` simulation steps (SO(3) PD low level + rigid-body dynamics) ---------
+ * f_des: B x 3n held constant over the steps, or NULL to use the last control step's output. */
+int dat_rollout(dat_handle* h, int steps, const double* f_des);
+
+/* ---- device-resident closed loop: hl_steps x (desired acceleration + control step +
+ * hl_every rollout steps); inputs already in HBM, nothing copied per step. */
+int dat_closed_loop(dat_handle* h, int hl_steps);
+
+/* ---- counters since the last reset: agent-QP solves, IPM iterations, control steps,
+ * and the summed device time of the high-level kernels [ms] (HIP events on the handle stream). */
+int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* hl_steps, double* hl_kernel_ms);
+int dat_reset_counters(dat_handle* h);
+int dat_synchronize(dat_handle* h);
+
+/* ---- raw batched kernels (tests / benchmarking of single pieces) ---------------------------
+ * Env CBF rows for every (scenario, agent) of the current state: lhs B x n x 10 x 3, rhs
+ * B x n x 10, nrow B x n, collision B x n, min_dist B x n (agent = -1 row when centralized). */
+int dat_env_rows(dat_handle* h, double* lhs, double* rhs, int* nrow, unsigned char* collision, double* min_dist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DAT_H */

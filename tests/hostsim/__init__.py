@@ -1,0 +1,81 @@
+"""ctypes loader for the TEST-ONLY host build of the per-lane device functions (see hostsim.hip)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libdat_hostsim.so")
+SRC = os.path.join(HERE, "hostsim.hip")
+CORE = os.path.join(os.path.dirname(os.path.dirname(HERE)), "distributed_aerial_transportation_amd", "csrc")
+
+
+def build(force=False):
+    deps = [SRC] + [os.path.join(CORE, f) for f in ("dat_core.hpp", "dat_layout.h")]
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(d) for d in deps):
+        subprocess.check_call(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
+                               SRC, "-o", LIB])
+    return LIB
+
+
+_lib = None
+D = ctypes.POINTER(ctypes.c_double)
+I = ctypes.POINTER(ctypes.c_int)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(LIB)
+    return _lib
+
+
+def p(a):
+    return np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(D)
+
+
+def qp_cadmm(prm, n, st, acc, lhs, rhs, i, lam, fbar, rho=1.0):
+    f = np.zeros(3 * n)
+    it = ctypes.c_int()
+    lhs = np.ascontiguousarray(lhs, dtype=np.float64).reshape(-1, 3)
+    status = lib().hs_qp_cadmm(p(prm), n, p(st), p(acc), p(lhs), p(rhs), lhs.shape[0], i, p(lam), p(fbar),
+                               ctypes.c_double(rho), f.ctypes.data_as(D), ctypes.byref(it))
+    return f, status, it.value
+
+
+def qp_dd(prm, n, st, acc, lhs, rhs, i, c9):
+    x = np.zeros(9)
+    it = ctypes.c_int()
+    lhs = np.ascontiguousarray(lhs, dtype=np.float64).reshape(-1, 3)
+    status = lib().hs_qp_dd(p(prm), n, p(st), p(acc), p(lhs), p(rhs), lhs.shape[0], i, p(c9), x.ctypes.data_as(D),
+                            ctypes.byref(it))
+    return x, status, it.value
+
+
+def qp_cent(prm, n, st, acc, lhs, rhs):
+    f = np.zeros(3 * n)
+    it = ctypes.c_int()
+    lhs = np.ascontiguousarray(lhs, dtype=np.float64).reshape(-1, 3)
+    status = lib().hs_qp_cent(p(prm), n, p(st), p(acc), p(lhs), p(rhs), lhs.shape[0], f.ctypes.data_as(D),
+                              ctypes.byref(it))
+    return f, status, it.value
+
+
+def env_rows(prm, n, st, trees, agent, alpha):
+    lhs = np.zeros((10, 3))
+    rhs = np.zeros(10)
+    col = ctypes.c_int()
+    md = ctypes.c_double()
+    trees = np.ascontiguousarray(trees, dtype=np.float64)
+    k = lib().hs_env_rows(p(prm), n, p(st), p(trees), trees.shape[0], agent, ctypes.c_double(alpha),
+                          lhs.ctypes.data_as(D), rhs.ctypes.data_as(D), ctypes.byref(col), ctypes.byref(md))
+    return lhs[:k], rhs[:k], bool(col.value), md.value
+
+
+def sim_step(prm, n, st, counter, fdes, dt):
+    st = np.array(st, dtype=np.float64)
+    c = ctypes.c_int(counter)
+    lib().hs_sim_step(p(prm), n, st.ctypes.data_as(D), ctypes.byref(c), p(fdes), ctypes.c_double(dt))
+    return st, c.value

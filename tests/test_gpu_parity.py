@@ -1,0 +1,219 @@
+"""GPU parity: the HIP path (libdat.so through the C-ABI) against the CPU oracle and the golden
+fixtures produced by the reference's own code.  Run with ``-m gpu`` on an MI355X.
+
+Tolerances (north_star): per-step controls within 1e-5 relative (relative to the largest force
+component of the step), closed-loop states within 1e-4.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import controllers as oc
+from oracle import forest as of
+from oracle import model as om
+from oracle import scenarios as osc
+from tests._golden import load, state_from, unpack_flat
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+
+
+def _eng(mode, n, B, **kw):
+    from distributed_aerial_transportation_amd import BatchedController, scenarios
+
+    return BatchedController(mode, n, B, scenarios.params_block(n), **kw)
+
+
+def _ostate(x, n):
+    from distributed_aerial_transportation_amd.system import RQPState
+
+    s = RQPState.unpack(x, n)
+    return om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def test_gpu_env_rows_match_oracle():
+    from distributed_aerial_transportation_amd import system as S
+
+    d = load("ref_env_rows.npz")
+    K = d["lhs_d"].shape[0]
+    states = np.stack([S.pack_state(state_from(d, "s_", k)) for k in range(K)])
+    eng = _eng("cadmm", 3, K)
+    f = of.Forest.__new__(of.Forest)
+    f.tree_pos = d["tree_pos"]
+    f.num_trees = f.tree_pos.shape[0]
+    f.mountain_center, f.mountain_radius = of.MOUNTAIN_CENTER, of.MOUNTAIN_RADIUS
+    f.mountain_sphere_radius, f.mountain_center_depth = 87.0, 83.3
+    eng.set_forests([f])
+    eng.set_state(states)
+    lhs, rhs, nr, col, md = eng.env_rows()
+    for k in range(K):
+        for i in range(3):
+            L, R = d["lhs_d"][k, i], d["rhs_d"][k, i]
+            keep = np.any(np.abs(L) > 1e-12, axis=1) | (R > 0)
+            exp = sorted(map(tuple, np.column_stack([L[keep], R[keep]])))
+            gl, gr = lhs[k, i, : nr[k, i]], rhs[k, i, : nr[k, i]]
+            keep2 = np.any(np.abs(gl) > 1e-12, axis=1) | (gr > 0)
+            got = sorted(map(tuple, np.column_stack([gl[keep2], gr[keep2]])))
+            assert len(got) == len(exp)
+            if got:
+                np.testing.assert_allclose(np.array(got), np.array(exp), atol=1e-9)
+            assert bool(col[k, i]) == bool(d["col_d"][k, i])
+            assert md[k, i] == pytest.approx(float(d["md_d"][k, i]), abs=1e-8)
+
+
+@pytest.mark.parametrize("n", [3, 6])
+def test_gpu_cadmm_step_matches_oracle(n):
+    from distributed_aerial_transportation_amd import scenarios
+
+    B = 6
+    rng = np.random.default_rng(n)
+    states = scenarios.perturbed_states(n, B, rng)
+    acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
+    eng = _eng("cadmm", n, B, record_err=True)
+    # two consecutive steps exercise the warm start (f, f_mean, lambda persist)
+    r1 = eng.control(states, acc)
+    r2 = eng.control(states, acc[::-1].copy())
+    for b in range(B):
+        ctl = oc.CADMM(osc.params(n), osc.col_radius(n))
+        s = _ostate(states[b], n)
+        f1, st1 = ctl.control(s, (acc[b, :3], acc[b, 3:]))
+        f2, st2 = ctl.control(s, (acc[B - 1 - b, :3], acc[B - 1 - b, 3:]))
+        assert r1.iters[b] == st1.iter and r2.iters[b] == st2.iter
+        assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL
+        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=1e-4, atol=1e-6)
+        assert np.all(r1.qp_status[b] == 0)
+
+
+def test_gpu_cadmm_convergence_recipe_golden():
+    """_plot_convergence_rate (test/control/test_rqpcontrollers.py:101-124): tol 0, 25 iterations,
+    aggregate residual -- against the reference's own loop (ref_cadmm.npz)."""
+    from distributed_aerial_transportation_amd import scenarios, system
+
+    d = load("ref_cadmm.npz")
+    eng = _eng("cadmm", 3, 1, record_err=True)
+    eng.set_force_err_tolerance(0.0, False)
+    eng.set_max_iter(25)
+    x = system.pack_state(scenarios.rest_state(3))[None]
+    for k in range(d["fixed_err"].shape[0]):
+        a = d["acc"][k][None]
+        r = eng.control(x, a)
+        assert r.iters[0] == 26
+        np.testing.assert_allclose(r.err_seq[0, :25], d["fixed_err"][k], rtol=1e-4, atol=1e-7)
+        assert _rel(r.f_des[0], d["fixed_f"][k]) < REL
+
+
+def test_gpu_cadmm_default_tolerance_golden():
+    from distributed_aerial_transportation_amd import scenarios, system
+
+    d = load("ref_cadmm.npz")
+    eng = _eng("cadmm", 3, 1)
+    x = system.pack_state(scenarios.rest_state(3))[None]
+    for k in range(d["tol_iters"].shape[0]):
+        r = eng.control(x, d["acc"][k][None])
+        assert r.iters[0] == d["tol_iters"][k]
+        assert _rel(r.f_des[0], d["tol_f"][k]) < REL
+
+
+@pytest.mark.parametrize("n", [3, 6])
+def test_gpu_dd_step_matches_oracle(n):
+    from distributed_aerial_transportation_amd import scenarios
+
+    B = 4
+    rng = np.random.default_rng(10 + n)
+    states = scenarios.perturbed_states(n, B, rng)
+    acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
+    eng = _eng("dd", n, B)
+    r1 = eng.control(states, acc)
+    for b in range(B):
+        ctl = oc.DD(osc.params(n), osc.col_radius(n))
+        f1, st1 = ctl.control(_ostate(states[b], n), (acc[b, :3], acc[b, 3:]))
+        assert abs(int(r1.iters[b]) - st1.iter) <= 1
+        if r1.iters[b] == st1.iter:
+            assert _rel(r1.f_des[b], f1) < 1e-4
+
+
+def test_gpu_dd_golden():
+    from distributed_aerial_transportation_amd import scenarios, system
+
+    d = load("ref_dd.npz")
+    x = system.pack_state(scenarios.rest_state(3))[None]
+    eng = _eng("dd", 3, 1, record_err=True)
+    eng.set_force_err_tolerance(0.0)
+    eng.set_max_iter(25)
+    for k in range(d["fixed_err"].shape[0]):
+        r = eng.control(x, d["acc"][k][None])
+        np.testing.assert_allclose(r.err_seq[0, :25], d["fixed_err"][k], rtol=1e-3, atol=1e-6)
+        assert _rel(r.f_des[0], d["fixed_f"][k]) < 1e-4
+    eng = _eng("dd", 3, 1)
+    for k in range(d["tol_iters"].shape[0]):
+        r = eng.control(x, d["acc"][k][None])
+        assert r.iters[0] == d["tol_iters"][k]
+        assert _rel(r.f_des[0], d["tol_f"][k]) < 1e-4
+
+
+def test_gpu_centralized_golden():
+    from distributed_aerial_transportation_amd import scenarios, system
+
+    d = load("ref_central.npz")
+    eng = _eng("centralized", 3, d["f"].shape[0])
+    x = np.repeat(system.pack_state(scenarios.rest_state(3))[None], d["f"].shape[0], axis=0)
+    r = eng.control(x, d["acc"])
+    for k in range(d["f"].shape[0]):
+        assert _rel(r.f_des[k], d["f"][k]) < REL
+    assert np.all(r.iters == -1)
+
+
+def test_gpu_rollout_matches_oracle():
+    from distributed_aerial_transportation_amd import scenarios
+
+    n, B = 3, 5
+    rng = np.random.default_rng(3)
+    states = scenarios.perturbed_states(n, B, rng)
+    eng = _eng("cadmm", n, B)
+    eng.set_state(states, np.zeros(B, dtype=np.int32))
+    fdes = np.stack([np.vstack([rng.uniform(-1, 1, (2, n)), rng.uniform(4, 7, (1, n))]) for _ in range(B)])
+    eng.rollout(45, fdes)
+    got, cnt = eng.get_state()
+    p = osc.params(n)
+    for b in range(B):
+        s = _ostate(states[b], n)
+        for _ in range(45):
+            f, M = om.low_level_control(p, s, fdes[b])
+            s.integrate(*om.forward_dynamics(p, s, f, M), 1e-3)
+        g = _ostate(got[b], n)
+        for a in ("R", "w", "xl", "vl", "Rl", "wl"):
+            np.testing.assert_allclose(getattr(g, a), getattr(s, a), atol=1e-12)
+        assert cnt[b] == s.counter
+
+
+@pytest.mark.parametrize("tag,mode", [("cons", "cadmm"), ("dual", "dd"), ("cent", "centralized")])
+def test_gpu_closed_loop_golden(tag, mode):
+    """400 ms of rqp_example's loop (forest seed 0, HL every 10 steps) vs the reference's loop."""
+    from distributed_aerial_transportation_amd import Forest, scenarios, system
+
+    d = load("ref_closed_loop.npz")
+    eng = _eng(mode, 3, 1)
+    eng.set_forests([Forest.seeded(0)])
+    eng.set_state(system.pack_state(scenarios.rest_state(3))[None], np.zeros(1, dtype=np.int32))
+    steps = d[f"{tag}_states"].shape[0] // 10
+    for k in range(steps):
+        r = eng.control(None, None)  # forest desired-acceleration law on device
+        assert _rel(r.f_des[0], d[f"{tag}_f_des"][k]) < 1e-4, k
+        if mode != "centralized":
+            assert r.iters[0] == d[f"{tag}_iters"][k]
+        eng.rollout(10)
+        st, _ = eng.get_state()
+        ref = d[f"{tag}_states"][10 * k + 9]
+        assert np.max(np.abs(st[0] - _reorder(ref))) < 1e-4, k
+
+
+def _reorder(x, n=3):
+    """fixture states are (R (3,3,n) C-order, w (3,n), xl, vl, Rl, wl) -> dat_layout state block"""
+    from distributed_aerial_transportation_amd import system
+
+    return system.pack_state(unpack_flat(x, n))
