@@ -1,0 +1,178 @@
+"""Benchmark: agent-QP solves/s (node) + ms per control step, 6-quadrotor C-ADMM (BASELINE.json).
+
+Workload (per GPU): n = 6 C-ADMM in the forest environment, B = 65536
+closed-loop scenarios per GPU (weak scaling), 64 seeded forests (scenario s uses forest s mod 64),
+start xl = (U(-2,0), U(-10,10), 1.5), vl = (0.5, 0, 0).  One "step" = one high-level period of
+every scenario, fully on device: forest desired-acceleration law + C-ADMM control step (env CBF
+rows, up to 101 ADMM iterations of n agent QPs each) + 10 simulation steps (SO(3) PD + dynamics).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --n 6 --mode cadmm]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+The data path has no collective; torch.distributed (RCCL over xGMI when N > 1) is used for the
+barrier, the max-over-ranks time and an all-gather of the per-scenario metrics.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (AMD spec)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md
+# FP64 flops per IPM iteration of the reduced agent QP, executed count of the structured kernel
+# (DESIGN.md "Roofline accounting"): fixed part + per u-row part.
+FLOPS_PER_IPM_ITER = 7600.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=65536, help="scenarios per GPU")
+    ap.add_argument("--n", type=int, default=6)
+    ap.add_argument("--mode", default="cadmm")
+    ap.add_argument("--forests", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-s", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(n: int, budget_s: float):
+    """Oracle (numpy) C-ADMM on a bounded sample of the same workload, one core."""
+    from distributed_aerial_transportation_amd import Forest, scenarios
+    from distributed_aerial_transportation_amd.system import RQPState
+    from oracle import controllers as oc
+    from oracle import forest as of
+    from oracle import model as om
+    from oracle import scenarios as osc
+
+    rng = np.random.default_rng(123)
+    np.random.seed(0)
+    forest = of.Forest()
+    solves, t0, steps = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        x = scenarios.forest_start_states(n, 1, rng)[0]
+        s = RQPState.unpack(x, n)
+        st = om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
+        ctl = oc.CADMM(osc.params(n), osc.col_radius(n), forest)
+        acc, _, _ = oc.desired_acceleration_forest(st, forest)
+        _, stats = ctl.control(st, acc)
+        solves += stats.iter * n
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
+            "sample": f"oracle C-ADMM n={n} (numpy dense IPM), {steps} forest control steps from C4 start "
+                      f"states, {solves} agent QPs in {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+
+    n, B = args.n, args.batch
+    rng = np.random.default_rng(1000 + rank)
+    forests = [Forest.seeded(s) for s in range(args.forests)]
+    states = scenarios.forest_start_states(n, B, rng)
+    eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
+    eng.set_forests(forests, (np.arange(B) + rank * B) % len(forests))
+    eng.set_state(states, np.zeros(B, dtype=np.int32))
+    eng.closed_loop(args.warmup)
+    eng.reset_counters()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.closed_loop(args.steps)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    qps, ipm, hl_steps, hl_ms = eng.counters()
+    # per-scenario metrics of the last step (all-gathered over ranks: the only collective)
+    res = eng.control(None, None)
+    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
+    tot = np.array([qps, ipm, hl_ms, elapsed], dtype=np.float64)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor(tot, device=f"cuda:{local}")
+        mx = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        gm = torch.tensor(local_metrics, device=f"cuda:{local}")
+        gath = [torch.empty_like(gm) for _ in range(world)]
+        dist.all_gather(gath, gm)
+        all_metrics = torch.cat(gath).cpu().numpy()
+        qps_all, ipm_all = float(t[0]), float(t[1])
+        elapsed = float(mx[3])
+        hl_ms_rank0 = float(tot[2])
+    else:
+        all_metrics = local_metrics
+        qps_all, ipm_all, hl_ms_rank0 = float(qps), float(ipm), float(hl_ms)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    value = qps_all / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    launch_ms = hl_ms_rank0 / max(hl_steps, 1)
+    flops_launch = (ipm / max(hl_steps, 1)) * FLOPS_PER_IPM_ITER
+    achieved_tflops = flops_launch / (launch_ms * 1e-3) / 1e12
+    out = {
+        "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "agent-QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded forests 0..63, randomized C4 start states)",
+        "config": {"workload": f"C4: {args.mode} n={n}, forest env, {B} closed-loop scenarios per GPU",
+                   "n": n, "scenarios_per_gpu": B, "hl_every": 10, "dt": 1e-3, "parallelism": f"scenario-sharded x{world}"},
+        "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
+                  "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
+                  "hl_kernel_ms_per_step": launch_ms},
+        "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "k_cadmm", "flops_per_ipm_iter": FLOPS_PER_IPM_ITER},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

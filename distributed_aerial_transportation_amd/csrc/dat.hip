@@ -43,7 +43,7 @@ int fail(const std::string& m) {
 constexpr int NMAX = 16;        // largest team the kernels are compiled for
 constexpr int NMAX_DD = 8;      // DD master matrix is (6n)^2 in LDS
 constexpr int IPM_MAX_ITER = 50;
-constexpr double IPM_TOL = 1e-9;
+constexpr double IPM_TOL = 1e-10;
 
 struct KArgs {
   int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)

@@ -1115,6 +1115,17 @@ DAT_HD IPMOut ipm_solve(const QP<NB>& P, double y[NB][3], double w[6], int max_i
     for (int l = 0; l < ml; ++l) rsl[l] += dss_l[l] * dzs_l[l] - sig * mu;
     newton(rsk, rsl);
     double alpha = fmin(1.0, 0.99 * step_len());
+    // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
+    // backtrack until the complementarity gap decreases
+    const bool feasible = pres < 1e-8 * nh && dres < 1e-8 * nq;
+    for (int bt = 0; feasible && bt < 8; ++bt) {
+      double g = 0.0;
+      for (int k = 0; k < NB; ++k)
+        for (int j = 0; j < 9; ++j) g += (lamk[k][j] + alpha * dss_k[k][j]) * (lamk[k][j] + alpha * dzs_k[k][j]);
+      for (int l = 0; l < ml; ++l) g += (laml[l] + alpha * dss_l[l]) * (laml[l] + alpha * dzs_l[l]);
+      if (g <= gap * (1.0 - 0.01 * alpha)) break;
+      alpha *= 0.5;
+    }
     // update.  ds from the primal equation (keeps G y + s = h exact), dz = W^-1 dzs.
     for (int k = 0; k < NB; ++k) {
       double g[9], dz[9];

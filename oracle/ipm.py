@@ -265,6 +265,13 @@ def solve_qp(P, q, G, h, dims: ConeDims, A=None, b=None, tol=1e-11, max_iter=80)
         dzl = W @ dz
         amax = min(_max_step(lam, dsl, dims), _max_step(lam, dzl, dims))
         alpha = min(1.0, 0.99 * amax)
+        # Safeguard: on a (nearly) feasible iterate Mehrotra's corrector can increase the gap and
+        # cycle; backtrack until the complementarity gap decreases.
+        if pres < 1e-8 and dres < 1e-8:
+            for _ in range(8):
+                if (lam + alpha * dsl) @ (lam + alpha * dzl) <= gap * (1.0 - 0.01 * alpha):
+                    break
+                alpha *= 0.5
         x = x + alpha * dx
         y = y + alpha * dy
         z = z + alpha * dz

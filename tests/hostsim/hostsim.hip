@@ -8,6 +8,10 @@
 
 using namespace dat;
 
+#ifndef HS_TOL
+#define HS_TOL 1e-10
+#endif
+
 extern "C" {
 
 int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
@@ -21,7 +25,7 @@ int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, c
   add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
   build_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_CADMM, 1>(P, y, w, 50, 1e-9);
+  IPMOut o = ipm_solve<MODE_CADMM, 1>(P, y, w, 50, HS_TOL);
   cadmm_materialize(P, n, i, Rt_all, lam, fbar, y[0], o.pi, f_out);
   *iters = o.iters;
   return o.status;
@@ -36,7 +40,7 @@ int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, cons
   set_dd_price(P, prm, n, i, c9);
   add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_DD, 1>(P, y, w, 50, 1e-9);
+  IPMOut o = ipm_solve<MODE_DD, 1>(P, y, w, 50, HS_TOL);
   for (int c = 0; c < 3; ++c) x_out[c] = y[0][c];
   for (int c = 0; c < 6; ++c) x_out[3 + c] = w[c];
   *iters = o.iters;
@@ -52,7 +56,7 @@ int hs_qp_cent(const double* prm, int n, const double* st, const double* acc, co
     build_cent(P, prm, n, st, acc);
     add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
     double y[3][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, 3>(P, y, w, 50, 1e-9);
+    IPMOut o = ipm_solve<MODE_CENT, 3>(P, y, w, 50, HS_TOL);
     for (int k = 0; k < 3; ++k)
       for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
     *iters = o.iters;
@@ -62,7 +66,7 @@ int hs_qp_cent(const double* prm, int n, const double* st, const double* acc, co
     build_cent(P, prm, n, st, acc);
     add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
     double y[6][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, 6>(P, y, w, 50, 1e-9);
+    IPMOut o = ipm_solve<MODE_CENT, 6>(P, y, w, 50, HS_TOL);
     for (int k = 0; k < 6; ++k)
       for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
     *iters = o.iters;
