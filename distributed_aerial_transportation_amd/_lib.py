@@ -16,7 +16,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libdat.so")
 SRC = os.path.join(PKG, "csrc", "dat.hip")
-DEPS = [SRC, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_layout.h"),
+DEPS = [SRC, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_qp.hpp"),
+        os.path.join(PKG, "csrc", "dat_layout.h"),
         os.path.join(REPO, "include", "dat.h")]
 
 MODE_CENTRALIZED, MODE_CADMM, MODE_DD = 0, 1, 2

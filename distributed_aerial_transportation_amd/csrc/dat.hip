@@ -21,7 +21,7 @@
 #include <vector>
 
 #include "../../include/dat.h"
-#include "dat_core.hpp"
+#include "dat_qp.hpp"
 
 using namespace dat;
 
@@ -88,6 +88,34 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 // ------------------------------------------------------------------------------------------------
 // C-ADMM
 // ------------------------------------------------------------------------------------------------
+// LDS layout of one 64-lane block (G = floor(64/n) scenarios):
+//   fx   NT x 3n   agent copies f^(i)            fbar G x 3n   consensus mean
+//   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x 8   per-lane exchange slots
+//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)   env 64 x EnvRows   done G ints
+struct CadmmLds {
+  double *fx, *fbar, *Rt, *red;
+  QPShared* sh;
+  EnvRows* env;
+  int* done;
+};
+__host__ __device__ inline size_t cadmm_lds_bytes(int n) {
+  const int G = 64 / n, NT = G * n;
+  return sizeof(double) * ((size_t)NT * 3 * n + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * 8) +
+         sizeof(QPShared) * (size_t)G + sizeof(EnvRows) * 64 + sizeof(int) * 64;
+}
+__device__ inline CadmmLds cadmm_carve(double* smem, int n) {
+  const int G = 64 / n, NT = G * n;
+  CadmmLds L;
+  L.fx = smem;
+  L.fbar = L.fx + NT * 3 * n;
+  L.Rt = L.fbar + G * 3 * n;
+  L.red = L.Rt + G * 9 * n;
+  L.sh = (QPShared*)(L.red + 64 * 8);
+  L.env = (EnvRows*)(L.sh + G);
+  L.done = (int*)(L.env + 64);
+  return L;
+}
+
 __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
@@ -96,17 +124,14 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   const int ls = lane / n, i = lane - ls * n;
   const int sc = blockIdx.x * G + ls;
   const bool valid = (lane < NT) && (sc < a.B);
-  double* fx = smem;                       // NT x 3n   agent copies f^(i)
-  double* fbar = fx + NT * N3;             // G x 3n    consensus mean
-  double* Rt = fbar + G * N3;              // G x 9n    hat(r_com_j) Rl'
-  double* red = Rt + G * 9 * n;            // 64 x 16   per-lane scratch
-  int* done = (int*)(red + 64 * 16);       // G
-  double* myf = fx + lane * N3;
-  double* fb = fbar + ls * N3;
-  double* rts = Rt + ls * 9 * n;
-  double* myred = red + lane * 16;
+  CadmmLds L = cadmm_carve(smem, n);
+  double* myf = L.fx + lane * N3;
+  double* fb = L.fbar + ls * N3;
+  double* rts = L.Rt + ls * 9 * n;
+  double* myred = L.red + lane * 8;
+  QPShared& S = L.sh[ls < G ? ls : 0];
 
-  QP<1> P;
+  QPLane<1> P;
   const double* prm = nullptr;
   double* lam = nullptr;
   int iter = 0, qstat = ST_OPTIMAL;
@@ -121,35 +146,45 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     for (int c = 0; c < N3; ++c) myf[c] = a.cf[((size_t)sc * n + i) * N3 + c];
     for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
     lam = a.clam + ((size_t)sc * n + i) * N3;
-    if (i == 0) done[ls] = 0;
+    if (i == 0) {
+      L.done[ls] = 0;
+      build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+    }
   } else if (lane < NT && i == 0) {
-    done[ls] = 1;
+    L.done[ls] = 1;
   }
   __syncthreads();
   if (valid) {
     const double* st = a.state + (size_t)sc * a.S;
-    build_cadmm_static(P, prm, n, st, a.acc + (size_t)sc * 6, i, rts);
+    lane_cadmm_static(P, prm, n, i, rts + 9 * i);
     const double* trees;
-    int nt, nrow = 0;
+    int nt;
+    unsigned emask;
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &nrow, lhs, rhs);
-    add_env_rows(P, nrow, lhs, rhs);
+    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+    set_env_rows(P, L.env[lane], S, emask, lhs, rhs);
   }
+  const LdsRef<QPShared> shr{L.sh, ls < G ? ls : 0};
+  const LdsRef<EnvRows> err{L.env, lane};
   double rho = a.rho0;
   for (;;) {
-    const bool active = valid && !done[ls];
+    const bool active = valid && !L.done[ls];
     if (active) {
-      build_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
+      lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_CADMM, 1>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ipm_solve<MODE_CADMM, 1>(shr, err, P, y, w, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
       ++my_qp;
       qstat = o.status;
       if (o.status == ST_OPTIMAL) {
-        double fnew[3 * NMAX];
-        cadmm_materialize(P, n, i, rts, lam, fb, y[0], o.pi, fnew);
-        for (int c = 0; c < N3; ++c) myf[c] = fnew[c];
+        for (int j = 0; j < n; ++j) {
+          if (j == i) {
+            myf[3 * j] = y[0][0]; myf[3 * j + 1] = y[0][1]; myf[3 * j + 2] = y[0][2];
+          } else {
+            cadmm_free_block(rts + 9 * j, lam + 3 * j, fb + 3 * j, o.pi, rho, myf + 3 * j);
+          }
+        }
       } else if (o.status == ST_FAILED) {  // solver exception -> f_eq (control/rqp_cadmm.py:491-494)
         for (int c = 0; c < N3; ++c) myf[c] = prm[DAT_P_FEQ(n) + c];
       }  // otherwise hold the previous solution (control/rqp_cadmm.py:496-499)
@@ -161,13 +196,13 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
       // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
       for (int c = 0; c < 3; ++c) {
         double s = 0.0;
-        for (int k = 0; k < n; ++k) s += fx[(ls * n + k) * N3 + 3 * i + c];
-        myred[8 + c] = s / n;
+        for (int k = 0; k < n; ++k) s += L.fx[(ls * n + k) * N3 + 3 * i + c];
+        myred[c] = s / n;
       }
     }
     __syncthreads();
     if (active) {
-      for (int c = 0; c < 3; ++c) fb[3 * i + c] = myred[8 + c];
+      for (int c = 0; c < 3; ++c) fb[3 * i + c] = myred[c];
     }
     __syncthreads();
     if (active) {
@@ -178,65 +213,50 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
           for (int j = 0; j < n; ++j) s += fabs(myf[3 * j + r] - fb[3 * j + r]);
           rmax = fmax(rmax, s);
         }
-        myred[0] = rmax;
+        myred[6] = rmax;
       } else {
-        // aggregate residual (control/rqp_cadmm.py:602-621)
-        double F[3] = {0, 0, 0}, M[3] = {0, 0, 0}, mi[3];
+        // aggregate residual (control/rqp_cadmm.py:602-621): own copy's totals of the others
+        double F[3] = {0, 0, 0}, M[3] = {0, 0, 0};
         for (int j = 0; j < n; ++j) {
+          if (j == i) continue;
           double m3[3];
           mv3(rts + 9 * j, myf + 3 * j, m3);
-          if (j == i) {
-            mi[0] = m3[0]; mi[1] = m3[1]; mi[2] = m3[2];
-            continue;
-          }
           for (int c = 0; c < 3; ++c) { F[c] += myf[3 * j + c]; M[c] += m3[c]; }
         }
-        for (int c = 0; c < 3; ++c) {
-          myred[1 + c] = F[c];
-          myred[4 + c] = M[c];
-          myred[11 + c] = myf[3 * i + c];  // f_app
+        // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
+        for (int k = 0; k < n; ++k) {
+          if (k == i) continue;
+          const double* fk = L.fx + (ls * n + k) * N3 + 3 * k;  // f_app_k = agent k's own block
+          double m3[3];
+          mv3(rts + 9 * k, fk, m3);
+          for (int c = 0; c < 3; ++c) { F[c] -= fk[c]; M[c] -= m3[c]; }
         }
-        (void)mi;
-      }
-    }
-    __syncthreads();
-    if (active && !a.use_total_res) {
-      // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
-      double sf[3] = {0, 0, 0}, sm[3] = {0, 0, 0};
-      for (int k = 0; k < n; ++k) {
-        if (k == i) continue;
-        const double* fk = red + (ls * n + k) * 16 + 11;
-        double m3[3];
-        mv3(rts + 9 * k, fk, m3);
-        for (int c = 0; c < 3; ++c) { sf[c] += fk[c]; sm[c] += m3[c]; }
-      }
-      for (int c = 0; c < 3; ++c) {
-        myred[1 + c] -= sf[c];
-        myred[4 + c] -= sm[c];
+        for (int c = 0; c < 3; ++c) { myred[c] = F[c]; myred[3 + c] = M[c]; }
       }
     }
     __syncthreads();
     if (active && i == 0) {
       double res = 0.0;
+      const double* rg = L.red + (ls * n) * 8;
       if (a.use_total_res) {
-        for (int k = 0; k < n; ++k) res = fmax(res, red[(ls * n + k) * 16]);
+        for (int k = 0; k < n; ++k) res = fmax(res, rg[8 * k + 6]);
       } else {
         for (int r = 0; r < 3; ++r) {
           double sF = 0.0, sM = 0.0;
           for (int k = 0; k < n; ++k) {
-            sF += fabs(red[(ls * n + k) * 16 + 1 + r]);
-            sM += fabs(red[(ls * n + k) * 16 + 4 + r]);
+            sF += fabs(rg[8 * k + r]);
+            sM += fabs(rg[8 * k + 3 + r]);
           }
           res = fmax(res, fmax(sF, sM));
         }
       }
       bool stop = (res < a.res_tol) || (iter > a.max_iter);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
-      red[(ls * n) * 16 + 15] = stop ? 1.0 : 0.0;
+      L.red[(ls * n) * 8 + 7] = stop ? 1.0 : 0.0;
     }
     __syncthreads();
     if (active) {
-      bool stop = red[(ls * n) * 16 + 15] != 0.0;
+      bool stop = L.red[(ls * n) * 8 + 7] != 0.0;
       if (!stop) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
       }
@@ -244,8 +264,8 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     __syncthreads();
     int any = 0;
     if (active && i == 0) {
-      bool stop = red[(ls * n) * 16 + 15] != 0.0;
-      done[ls] = stop ? 1 : 0;
+      bool stop = L.red[(ls * n) * 8 + 7] != 0.0;
+      L.done[ls] = stop ? 1 : 0;
       any = stop ? 0 : 1;
     }
     if (!__syncthreads_or(any)) break;
@@ -267,8 +287,8 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     int coll = 0;
     double md = prm[DAT_P_VISR];
     for (int k = 0; k < n; ++k) {
-      coll |= red[(ls * n + k) * 16] != 0.0;
-      md = fmin(md, red[(ls * n + k) * 16 + 1]);
+      coll |= L.red[(ls * n + k) * 8] != 0.0;
+      md = fmin(md, L.red[(ls * n + k) * 8 + 1]);
     }
     a.col[sc] = (unsigned char)coll;
     a.mind[sc] = md;
@@ -440,12 +460,15 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* E = lamM + G * N3;        // NT x 6   consensus error
   double* Rts = E + NT * 6;         // G x 9n
   double* red = Rts + G * 9 * n;    // 64 x 4
+  QPShared* shs = (QPShared*)(red + 64 * 4);  // G
+  EnvRows* envs = (EnvRows*)(shs + G);        // 64
+  QPShared& S = shs[ls < G ? ls : 0];
   double* myX = X + lane * 9;
   double* lF = lamF + ls * N3;
   double* lM = lamM + ls * N3;
   double* rts = Rts + ls * 9 * n;
 
-  QP<1> P;
+  QPLane<1> P;
   const double* prm = nullptr;
   double prev[9];
   int iter = 0, qstat = ST_OPTIMAL;
@@ -462,16 +485,23 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
     }
     for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
-    build_dd_static(P, prm, n, st, a.acc + (size_t)sc * 6, i, rts + 9 * i);
-    const double* trees;
-    int nt, nrow = 0;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &nrow, lhs, rhs);
-    add_env_rows(P, nrow, lhs, rhs);
+    if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
   }
   if (lane < 64) red[lane * 4 + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
   __syncthreads();
+  if (valid) {
+    const double* st = a.state + (size_t)sc * a.S;
+    lane_dd_static(P, prm, n, i, rts + 9 * i);
+    const double* trees;
+    int nt;
+    unsigned emask;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+    set_env_rows(P, envs[lane], S, emask, lhs, rhs);
+  }
+  const LdsRef<QPShared> shr{shs, ls < G ? ls : 0};
+  const LdsRef<EnvRows> err{envs, lane};
   const double* Rl = valid ? a.state + (size_t)sc * a.S + DAT_S_RL(n) : nullptr;
   for (;;) {
     const bool active = valid && red[(ls * n) * 4 + 3] == 0.0;
@@ -491,7 +521,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       }
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_DD, 1>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ipm_solve<MODE_DD, 1>(shr, err, P, y, w, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
       ++my_qp;
       qstat = o.status;
@@ -610,16 +640,20 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     const int n = NB;
     const double* prm = prm_of(a, sc);
     const double* st = a.state + (size_t)sc * a.S;
-    QP<NB> P;
-    build_cent<NB>(P, prm, n, st, a.acc + (size_t)sc * 6);
+    QPShared S;
+    build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
+    QPLane<NB> P;
+    lane_cent<NB>(P, prm, n, st);
     const double* trees;
-    int nt, nrow = 0;
+    int nt;
+    unsigned emask;
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    EnvOut env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &nrow, lhs, rhs);
-    add_env_rows(P, nrow, lhs, rhs);
+    EnvOut env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &emask, lhs, rhs);
+    EnvRows E;
+    set_env_rows(P, E, S, emask, lhs, rhs);
     double y[NB][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, NB>(P, y, w, IPM_MAX_ITER, IPM_TOL);
+    IPMOut o = ipm_solve<MODE_CENT, NB>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, IPM_MAX_ITER, IPM_TOL);
     q = 1;
     ip = o.iters;
     double* pf = a.pf + (size_t)sc * 3 * n;
@@ -716,13 +750,23 @@ __global__ void k_env(KArgs a, double* lhs, double* rhs, int* nrow, unsigned cha
   const double* st = a.state + (size_t)sc * a.S;
   const double* trees;
   int nt, k = 0;
+  unsigned mask;
   forest_of(a, sc, &trees, &nt);
   double L[DAT_NENV][3], R[DAT_NENV];
   bool cent = (a.cf == nullptr && a.dlamF == nullptr);
-  EnvOut e = env_rows(prm, n, st, trees, nt, cent ? -1 : i, cent ? prm[DAT_P_AENVC] : prm[DAT_P_AENVD], &k, L, R);
+  EnvOut e = env_rows(prm, n, st, trees, nt, cent ? -1 : i, cent ? prm[DAT_P_AENVC] : prm[DAT_P_AENVD], &mask, L, R);
+  double* lo = lhs + (size_t)t * DAT_NENV * 3;
+  double* ro = rhs + (size_t)t * DAT_NENV;
   for (int r = 0; r < DAT_NENV; ++r) {
-    for (int c = 0; c < 3; ++c) lhs[((size_t)t * DAT_NENV + r) * 3 + c] = r < k ? L[r][c] : 0.0;
-    rhs[(size_t)t * DAT_NENV + r] = r < k ? R[r] : 0.0;
+    for (int c = 0; c < 3; ++c) lo[3 * r + c] = 0.0;
+    ro[r] = 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < DAT_NENV; ++r) {
+    if (!((mask >> r) & 1u)) continue;
+    for (int c = 0; c < 3; ++c) lo[3 * k + c] = L[r][c];
+    ro[k] = R[r];
+    ++k;
   }
   nrow[t] = k;
   col[t] = (unsigned char)e.collision;
@@ -823,13 +867,10 @@ KArgs kargs(dat_handle* h) {
   return a;
 }
 
-size_t cadmm_lds(int n) {
-  int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * 3 * n + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * 16) + sizeof(int) * 64;
-}
 size_t dd_lds(int n) {
   int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * 6 + (size_t)G * 9 * n + 64 * 4);
+  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * 6 + (size_t)G * 9 * n + 64 * 4) +
+         sizeof(QPShared) * (size_t)G + sizeof(EnvRows) * 64;
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
@@ -846,7 +887,7 @@ int launch_hl(dat_handle* h) {
   if (h->cfg.mode == DAT_MODE_CADMM) {
     int G = 64 / n;
     int blocks = (B + G - 1) / G;
-    hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds(n), h->stream, a);
+    hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(n), h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
     int G = 64 / n;
@@ -955,7 +996,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     return fail(m);
   }
   // LDS budgets
-  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
+  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
   if (lds > 160 * 1024) {
     dat_destroy(h);
     return fail("dat_create: LDS budget exceeded");

@@ -1,0 +1,1097 @@
+// dat_qp.hpp -- the reduced agent QP and its interior-point solver (per-lane fp64 device code).
+//
+// Data placement (DESIGN.md "Register and LDS budget"):
+//   QPShared   everything that is the same for all agents of one scenario (u-maps, the packed
+//              u-space Hessians, the base rows, the C-ADMM aggregate K).  The C-ADMM / DD kernels
+//              keep one copy per scenario in LDS; the centralized kernel keeps it in registers.
+//   QPLane     the agent's own data (cone block constants, env rows, linear terms) in registers.
+// Every array the solver touches is indexed with compile-time indices only (rows are fixed slots
+// with an activity mask, loops are unrolled, the LU row exchange is a predicated swap), so
+// nothing is demoted to scratch memory.
+//
+// u = (S, Mo) in R^6: aggregate force and moment about the CoM in payload axes,
+//   S = sum_j f_j,  Mo = sum_j hat(r_com_j) Rl' f_j      (control/rqp_cadmm.py:376-392)
+// Accelerations are affine in u:
+//   dwl = JT^-1 Mo + bw,           bw = -JT^-1 (wl x JT wl)
+//   dvl = S/mT + Bv Mo + bv,       Bv = Rl hat(x_com) JT^-1,
+//                                  bv = -g e3 - Rl hat(wl)^2 x_com + Rl hat(x_com) bw
+// Cone block k (an agent's own force f_k in R^3): f_kz >= min_fz, ||f_k|| <= sec f_kz,
+// ||f_k|| <= max_f.  Row slots (affine in (dvl, dwl)):  0 tilt (dwl), 1 |wl| (dwl), 2 |vl| (dvl),
+// 3 .. 3+DAT_NENV-1 env CBFs (dvl).
+#pragma once
+
+#include "dat_core.hpp"
+
+namespace dat {
+
+#ifndef DAT_IPM_NROW
+#define DAT_IPM_NROW DAT_MAXROW
+#endif
+constexpr int NROW = DAT_IPM_NROW;  // row slots processed by the solver (tools/micro overrides it)
+constexpr int NWROW = 2;          // slots [0, NWROW) act on dwl
+constexpr int NBASE = 3;          // base slots shared by all agents of a scenario
+
+struct QPShared {
+  double inv_mT, Bv[9], JTi[9], bv[3], bw[3];
+  double C[2][21];     // packed u-space Hessian: [0] without, [1] with the leader's desired-acc terms
+  double cu[2][6];     // matching linear terms
+  double K[21];        // C-ADMM: sum over ALL agents of U_j U_j' (agent i subtracts its own term)
+  double ba[NBASE][3]; // base rows: coefficients on dwl (slots 0, 1) or dvl (slot 2)
+  double bb[NBASE];    // constants (the affine offsets bw / bv folded in)
+  int bmask;           // active base slots
+  int infeasible;      // a dropped all-zero row had a negative constant
+};
+
+// env CBF rows of one agent (dvl): a . lin_v(u) + b >= 0 (kept in LDS by the kernels)
+struct EnvRows {
+  double a[DAT_NENV][3], b[DAT_NENV];
+};
+
+// Access to solver data kept outside the register file.  get() re-derives the reference through
+// an index the compiler cannot see through, so loads are issued where the data is consumed and
+// never hoisted out of the IPM loop or merged across uses (hoisting would pin ~150 doubles of
+// loop-invariant data in registers and spill the iterates).
+template <class T>
+struct PlainRef {
+  const T* p;
+  DAT_HD const T& get() const { return *p; }
+};
+template <class T>
+struct LdsRef {
+  const T* base;
+  int idx;
+  __device__ const T& get() const {
+    int j = idx;
+    __asm__ volatile("" : "+v"(j));
+    return base[j];
+  }
+};
+
+template <int NB>
+struct QPLane {
+  int var;                       // C / cu variant
+  unsigned emask;                // active env slots
+  int infeasible;
+  double kappa, rho, min_fz, max_f, sec;
+  double q[NB][3];               // per-block linear term
+  double y0[NB][3];              // interior initial guess (f_eq)
+  double Rt[NB][9];              // U_k = [I; Rt_k],  Rt_k = hat(r_com_k) Rl'
+  double atil[6];                // C-ADMM: sum_{j != i} U_j a_j
+  double cw[6];                  // DD: linear cost on w = (F_i, M_i)
+};
+
+// ------------------------------------------------------------------ shared data
+// k_f, k_m: total force / moment weights; variants: bit 0 build C[0] (kdv = 0), bit 1 build C[1]
+// (kdv = 1).  with_K: C-ADMM aggregate over all agents.
+DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st, const double* acc, double k_f,
+                         double k_m, int variants, bool with_K) {
+  const double mT = prm[DAT_P_MT];
+  const double* xc = prm + DAT_P_XCOM;
+  const double* JT = prm + DAT_P_JT;
+  const double* JTi = prm + DAT_P_JTI;
+  const double* Rl = st + DAT_S_RL(n);
+  const double* wl = st + DAT_S_WL(n);
+  const double* vl = st + DAT_S_VL(n);
+  S.inv_mT = 1.0 / mT;
+  for (int i = 0; i < 9; ++i) S.JTi[i] = JTi[i];
+  double Xh[9], RX[9];
+  skew3(xc, Xh);
+  mm3(Rl, Xh, RX);              // Rl hat(x_com)
+  mm3(RX, JTi, S.Bv);           // Rl hat(x_com) JT^-1
+  double Jw[3], wJw[3], bw[3], bv[3];
+  mv3(JT, wl, Jw);
+  cross3(wl, Jw, wJw);
+  mv3(JTi, wJw, bw);            // c_w = JT^-1 (wl x JT wl)
+  bw[0] = -bw[0]; bw[1] = -bw[1]; bw[2] = -bw[2];
+  // bv = -g e3 - Rl hat(wl)^2 x_com + Rl hat(x_com) bw
+  double wx[3], wwx[3], t1[3], t2[3];
+  cross3(wl, xc, wx);
+  cross3(wl, wx, wwx);
+  mv3(Rl, wwx, t1);
+  mv3(RX, bw, t2);
+  bv[0] = -t1[0] + t2[0];
+  bv[1] = -t1[1] + t2[1];
+  bv[2] = -DAT_GRAVITY - t1[2] + t2[2];
+  for (int c = 0; c < 3; ++c) { S.bw[c] = bw[c]; S.bv[c] = bv[c]; }
+
+  // Phi(u) = k_f ||S - mT g e3||^2 + k_m ||Mo||^2 + kdv (||dvl||^2 - 2 dvl_des'dvl)
+  //          + kdv (||dwl||^2 - 2 dwl_des'dwl)          (control/rqp_cadmm.py:436-458)
+  for (int v = 0; v < 2; ++v) {
+    if (!((variants >> v) & 1)) continue;
+    double* C = S.C[v];
+    double* cu = S.cu[v];
+    for (int k = 0; k < 21; ++k) C[k] = 0.0;
+    for (int r = 0; r < 3; ++r) { C[sp6(r, r)] = 2.0 * k_f; C[sp6(3 + r, 3 + r)] = 2.0 * k_m; }
+    for (int r = 0; r < 6; ++r) cu[r] = 0.0;
+    cu[2] = -2.0 * k_f * mT * DAT_GRAVITY;
+    if (v == 1) {
+      // Av = [I/mT, Bv], Aw = [0, JTi]: C += 2 (Av'Av + Aw'Aw)
+      const double im = S.inv_mT;
+      for (int r = 0; r < 3; ++r) {
+        C[sp6(r, r)] += 2.0 * im * im;
+        for (int c = 0; c < 3; ++c) C[sp6(r, 3 + c)] += 2.0 * im * S.Bv[3 * r + c];
+      }
+      for (int r = 0; r < 3; ++r)
+        for (int c = r; c < 3; ++c) {
+          double s = 0.0;
+          for (int k = 0; k < 3; ++k) s += S.Bv[3 * k + r] * S.Bv[3 * k + c] + JTi[3 * k + r] * JTi[3 * k + c];
+          C[sp6(3 + r, 3 + c)] += 2.0 * s;
+        }
+      double ev[3] = {bv[0] - acc[0], bv[1] - acc[1], bv[2] - acc[2]};
+      double ew[3] = {bw[0] - acc[3], bw[1] - acc[4], bw[2] - acc[5]};
+      double t[3], s3[3];
+      mtv3(S.Bv, ev, t);
+      mtv3(JTi, ew, s3);
+      for (int r = 0; r < 3; ++r) {
+        cu[r] += 2.0 * im * ev[r];
+        cu[3 + r] += 2.0 * (t[r] + s3[r]);
+      }
+    }
+  }
+  if (with_K) {
+    for (int k = 0; k < 21; ++k) S.K[k] = 0.0;
+    const double I3[6] = {1, 0, 0, 1, 0, 1};
+    for (int j = 0; j < n; ++j) {
+      double Rt[9];
+      make_Rt(prm + DAT_P_RCOM(n) + 3 * j, Rl, Rt);
+      add_UDUt(S.K, Rt, I3, 1.0);
+    }
+  }
+
+  // base rows (control/rqp_cadmm.py:406-430).  Tilt: (Rl hat(wl))[2,2] = Rl[2,:].(wl x e3),
+  // (Rl hat(wl)^2)[2,2] = Rl[2,:].(wl x (wl x e3)).
+  S.bmask = 0;
+  S.infeasible = 0;
+  double e3[3] = {0, 0, 1}, a[3], b[3];
+  cross3(wl, e3, a);
+  cross3(wl, a, b);
+  double al[NBASE][3] = {{-Rl[7], Rl[6], 0.0},
+                         {-2.0 * wl[0], -2.0 * wl[1], -2.0 * wl[2]},
+                         {-2.0 * vl[0], -2.0 * vl[1], -2.0 * vl[2]}};
+  double beta[NBASE] = {dot3(Rl + 6, b) + 2.0 * dot3(Rl + 6, a) + (Rl[8] - prm[DAT_P_COSP]),
+                        prm[DAT_P_MAXWL2] - dot3(wl, wl), prm[DAT_P_MAXVL2] - dot3(vl, vl)};
+  for (int l = 0; l < NBASE; ++l) {
+    for (int c = 0; c < 3; ++c) S.ba[l][c] = al[l][c];
+    if (al[l][0] == 0.0 && al[l][1] == 0.0 && al[l][2] == 0.0) {
+      if (beta[l] < 0.0) S.infeasible = 1;  // 0 >= -beta fails: the QP is infeasible
+      S.bb[l] = 1.0;                        // 0 >= 0 carries no information: padding row
+      continue;
+    }
+    S.bb[l] = beta[l] + dot3(al[l], l < NWROW ? bw : bv);
+    S.bmask |= 1 << l;
+  }
+}
+
+// env rows (dvl): lhs . dvl >= rhs  <=>  lhs . lin_v(u) + (lhs . bv - rhs) >= 0
+template <int NB>
+DAT_HD void set_env_rows(QPLane<NB>& P, EnvRows& E, const QPShared& S, unsigned mask, const double lhs[DAT_NENV][3],
+                         const double rhs[DAT_NENV]) {
+  P.emask = 0u;
+  P.infeasible = 0;
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) {
+    // inactive slots hold the padding row 0 . x + 1 >= 0
+    E.a[j][0] = 0.0; E.a[j][1] = 0.0; E.a[j][2] = 0.0;
+    E.b[j] = 1.0;
+    if (!((mask >> j) & 1u)) continue;
+    if (lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0) {
+      if (-rhs[j] < 0.0) P.infeasible = 1;
+      continue;
+    }
+    E.a[j][0] = lhs[j][0]; E.a[j][1] = lhs[j][1]; E.a[j][2] = lhs[j][2];
+    E.b[j] = -rhs[j] + dot3(lhs[j], S.bv);
+    P.emask |= 1u << j;
+  }
+}
+
+// ------------------------------------------------------------------ per-agent data
+template <int NB>
+DAT_HD void lane_common(QPLane<NB>& P, const double* prm) {
+  P.min_fz = prm[DAT_P_MINFZ];
+  P.max_f = prm[DAT_P_MAXF];
+  P.sec = prm[DAT_P_SEC];
+  P.emask = 0u;
+  P.infeasible = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) { P.atil[r] = 0.0; P.cw[r] = 0.0; }
+  P.rho = 1.0;
+}
+
+// C-ADMM agent i (control/rqp_cadmm.py:26-501): variables f in R^{3 x n} (agent i's full copy).
+// Cost: Phi(u) with k = 0.1/n, k_feq ||f_i - f_eq_i||^2, leader terms, <lam, f> + rho/2 ||f||^2
+// - <rho fbar, f>  ==  rho/2 ||f - a||^2 + const with a = fbar - lam / rho.
+// Only f_i carries cones; f_j (j != i) are free and eliminated through (K, atil).
+DAT_HD void lane_cadmm_static(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_i) {
+  lane_common(P, prm);
+  P.var = (i == 0) ? 1 : 0;
+#pragma unroll
+  for (int c = 0; c < 9; ++c) P.Rt[0][c] = Rt_i[c];
+  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) P.y0[0][c] = feq[c];
+}
+// per-iteration part: penalty rho and a = fbar - lam / rho.  lam, fbar: (3n) agent-major;
+// Rt_all: n x 9.
+DAT_HD void lane_cadmm_dynamic(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_all,
+                               const double* lam, const double* fbar, double rho) {
+  const double kfeq = prm[DAT_P_KFEQ];
+  const double irho = 1.0 / rho;
+  P.rho = rho;
+  P.kappa = 2.0 * kfeq + rho;
+  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) P.atil[r] = 0.0;
+  for (int j = 0; j < n; ++j) {
+    double a[3] = {fbar[3 * j] - lam[3 * j] * irho, fbar[3 * j + 1] - lam[3 * j + 1] * irho,
+                   fbar[3 * j + 2] - lam[3 * j + 2] * irho};
+    if (j == i) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) P.q[0][c] = -2.0 * kfeq * feq[c] - rho * a[c];
+    } else {
+      double t[6];
+      U_apply(Rt_all + 9 * j, a, t);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) P.atil[r] += t[r];
+    }
+  }
+}
+// agent i's copy of agent j != i: f_j = a_j - U_j' pi / rho  (stationarity of the free blocks)
+DAT_HD void cadmm_free_block(const double* Rt_j, const double* lam_j, const double* fbar_j, const double* pi,
+                             double rho, double* f_j) {
+  double t[3];
+  Ut_apply(Rt_j, pi, t);
+  const double irho = 1.0 / rho;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) f_j[c] = fbar_j[c] - (lam_j[c] + t[c]) * irho;
+}
+
+// DD agent i (control/rqp_dd.py:27-505): variables (f_i, F_i, M_i); with w = (F_i, M_i),
+// u = U_i f_i + w.  Cost Phi(u) + k_feq ||f_i - f_eq_i||^2 + c_fi'f_i + (c_Fi, c_Mi)'w.
+DAT_HD void lane_dd_static(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_i) {
+  lane_common(P, prm);
+  P.var = (i == 0) ? 1 : 0;
+#pragma unroll
+  for (int c = 0; c < 9; ++c) P.Rt[0][c] = Rt_i[c];
+  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) P.y0[0][c] = feq[c];
+  P.kappa = 2.0 * prm[DAT_P_KFEQ];
+}
+// prices c = (c_fi, c_Fi, c_Mi) (control/rqp_dd.py:718-722)
+DAT_HD void set_dd_price(QPLane<1>& P, const double* prm, int n, int i, const double* c9) {
+  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
+  const double kfeq = prm[DAT_P_KFEQ];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) P.q[0][c] = -2.0 * kfeq * feq[c] + c9[c];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) P.cw[r] = c9[3 + r];
+}
+
+// Centralized (control/rqp_centralized.py:27-448): all n agents' forces, k = 0.1, leader terms on.
+template <int NB>
+DAT_HD void lane_cent(QPLane<NB>& P, const double* prm, int n, const double* st) {
+  lane_common(P, prm);
+  P.var = 1;
+  const double kfeq = prm[DAT_P_KFEQ];
+  const double* Rl = st + DAT_S_RL(n);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const double* feq = prm + DAT_P_FEQ(n) + 3 * k;
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * k, Rl, P.Rt[k]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      P.y0[k][c] = feq[c];
+      P.q[k][c] = -2.0 * kfeq * feq[c];
+    }
+  }
+  P.kappa = 2.0 * kfeq;
+}
+
+// =====================================================================================
+// interior-point method on the reduced problem
+// =====================================================================================
+// Per cone block: slack/dual layout [fz | soc1 (4) | soc2 (4)] (9 entries),
+//   s = h - G y,  G y = -(y2, sec y2, y0, y1, y2, 0, y0, y1, y2),  h = (-min_fz, 0,0,0,0, max_f, 0,0,0).
+// Cone blocks use Nesterov-Todd scaling; the LP rows (u-slots) are carried unscaled (for the
+// nonnegative orthant NT scaling is diagonal and the two forms are algebraically identical).
+struct SocScale {
+  double w0, w1, w2, w3, eta, ieta, k1;  // k1 = 1 / (1 + w0)
+};
+
+DAT_HD double soc_det(const double* v) {
+  double n1 = sqrt(v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+  return (v[0] - n1) * (v[0] + n1);
+}
+DAT_HD bool soc_scaling(const double* s, const double* z, SocScale& S) {
+  double ds = soc_det(s), dz = soc_det(z);
+  if (!(ds > 0) || !(dz > 0)) return false;
+  double sn = sqrt(ds), zn = sqrt(dz);
+  double isn = frcp(sn), izn = frcp(zn);
+  double s0 = s[0] * isn, s1 = s[1] * isn, s2 = s[2] * isn, s3 = s[3] * isn;
+  double z0 = z[0] * izn, z1 = z[1] * izn, z2 = z[2] * izn, z3 = z[3] * izn;
+  double g = sqrt(0.5 * (1.0 + s0 * z0 + s1 * z1 + s2 * z2 + s3 * z3));
+  double ig = 0.5 * frcp(g);
+  S.w0 = (s0 + z0) * ig;
+  S.w1 = (s1 - z1) * ig;
+  S.w2 = (s2 - z2) * ig;
+  S.w3 = (s3 - z3) * ig;
+  S.eta = sqrt(sn * izn);
+  S.ieta = frcp(S.eta);
+  S.k1 = frcp(1.0 + S.w0);
+  return true;
+}
+// o = W v (inv = false) or W^-1 v (inv = true); W = eta H(w), W^-1 = H(Jw)/eta
+DAT_HD void soc_apply(const SocScale& S, const double* v, double* o, bool inv) {
+  const double sg = inv ? -1.0 : 1.0;
+  const double w1 = sg * S.w1, w2 = sg * S.w2, w3 = sg * S.w3;
+  const double wv = w1 * v[1] + w2 * v[2] + w3 * v[3];
+  const double k = v[0] + wv * S.k1;
+  const double sc = inv ? S.ieta : S.eta;
+  const double o0 = S.w0 * v[0] + wv;
+  o[1] = sc * (v[1] + k * w1);
+  o[2] = sc * (v[2] + k * w2);
+  o[3] = sc * (v[3] + k * w3);
+  o[0] = sc * o0;
+}
+// x = lam \ y (inverse Jordan product) for a 4-dim SOC
+DAT_HD void soc_jdiv(const double* l, const double* y, double* x) {
+  double det = l[0] * l[0] - (l[1] * l[1] + l[2] * l[2] + l[3] * l[3]);
+  double x0 = (l[0] * y[0] - (l[1] * y[1] + l[2] * y[2] + l[3] * y[3])) * frcp(det);
+  double il0 = frcp(l[0]);
+  x[0] = x0;
+  x[1] = (y[1] - x0 * l[1]) * il0;
+  x[2] = (y[2] - x0 * l[2]) * il0;
+  x[3] = (y[3] - x0 * l[3]) * il0;
+}
+DAT_HD void soc_jprod(const double* a, const double* b, double* o) {
+  double d = a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+  o[1] = a[0] * b[1] + b[0] * a[1];
+  o[2] = a[0] * b[2] + b[0] * a[2];
+  o[3] = a[0] * b[3] + b[0] * a[3];
+  o[0] = d;
+}
+// largest step a with x + a d in the SOC (1e300 if unbounded)
+DAT_HD double soc_step(const double* x, const double* d) {
+  double a = d[0] * d[0] - (d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);
+  double b = x[0] * d[0] - (x[1] * d[1] + x[2] * d[2] + x[3] * d[3]);
+  double n1 = sqrt(x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+  double c = (x[0] - n1) * (x[0] + n1);
+  double disc = b * b - a * c;
+  if (a < 0.0 || (b < 0.0 && disc >= 0.0)) {
+    double den = -b + sqrt(fmax(disc, 0.0));
+    return den > 0.0 ? c * frcp(den) : 0.0;
+  }
+  return 1e300;
+}
+
+struct IPMOut {
+  int status;
+  int iters;
+  double pi[6];   // u-space gradient C u + cu - A' z_rows at the solution
+  double u[6];
+};
+
+// Solve the reduced QP. MODE_CADMM: NB = 1, implicit free blocks through (K, atil, rho);
+// MODE_DD: NB = 1, w = (F_i, M_i) free with linear cost cw; MODE_CENT: NB = n, no w.
+// y (NB x 3) and w (6) are outputs.  sh / er: accessors of the scenario data and the env rows.
+//
+// Register economy (DESIGN.md "Register and LDS budget"): the row loops are branch-free over all
+// NROW slots (an inactive slot is the padding row 0 . x + 1 >= 0 with z = 0, whose complementarity
+// target is zeroed, so it never moves and adds exactly nothing); primal residuals and the scaled
+// cone residual are recomputed where consumed instead of being kept live.
+template <int MODE, int NB, class SH, class ER>
+DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double y[NB][3], double w[6], int max_iter,
+                        double tol) {
+  IPMOut out;
+  out.status = ST_FAILED;
+  out.iters = 0;
+  if (sh.get().infeasible || P.infeasible) {
+    out.status = ST_INFEASIBLE;
+    return out;
+  }
+  const unsigned mask = (unsigned)sh.get().bmask | (P.emask << NBASE);
+  const int var = P.var;
+  const double sec = P.sec, kap = P.kappa;
+  const double irho = 1.0 / P.rho;
+  const double im = sh.get().inv_mT;
+  auto act = [&](int l) -> double { return ((mask >> l) & 1u) ? 1.0 : 0.0; };
+  auto Cp = [&]() -> const double* { return sh.get().C[var]; };
+  auto cup = [&]() -> const double* { return sh.get().cu[var]; };
+  auto ra = [&](int l, int c) -> double {
+    return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.get().a[l >= NBASE ? l - NBASE : 0][c];
+  };
+  auto rb = [&](int l) -> double { return l < NBASE ? sh.get().bb[l < NBASE ? l : 0] : er.get().b[l >= NBASE ? l - NBASE : 0]; };
+  // row value a_l . (dvl or dwl) of the linear map of u
+  auto rowdot = [&](int l, const double* dv, const double* dw) -> double {
+    const double* x = l < NWROW ? dw : dv;
+    return ra(l, 0) * x[0] + ra(l, 1) * x[1] + ra(l, 2) * x[2];
+  };
+  auto lin = [&](const double* u, double* dv, double* dw) {
+    const QPShared& S = sh.get();
+    double t[3];
+    mv3(S.Bv, u + 3, t);
+    dv[0] = im * u[0] + t[0]; dv[1] = im * u[1] + t[1]; dv[2] = im * u[2] + t[2];
+    mv3(S.JTi, u + 3, dw);
+  };
+  auto adj = [&](const double* gv, const double* gw, double* o) {
+    const QPShared& S = sh.get();
+    double t[3], s[3];
+    mtv3(S.Bv, gv, t);
+    mtv3(S.JTi, gw, s);
+    o[0] = im * gv[0]; o[1] = im * gv[1]; o[2] = im * gv[2];
+    o[3] = t[0] + s[0]; o[4] = t[1] + s[1]; o[5] = t[2] + s[2];
+  };
+  auto rows_adj = [&](const double* zz, double* o) {  // o = A' zz (u-space)
+    double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0};
+#pragma unroll
+    for (int l = 0; l < NROW; ++l) {
+      double* g = l < NWROW ? gw : gv;
+      g[0] += zz[l] * ra(l, 0); g[1] += zz[l] * ra(l, 1); g[2] += zz[l] * ra(l, 2);
+    }
+    adj(gv, gw, o);
+  };
+  // K_{-i} v = K v - U_i (U_i' v)
+  auto Kmul = [&](const double* v, double* o) {
+    spmv6(sh.get().K, v, o);
+    double t[3], t6[6];
+    Ut_apply(P.Rt[0], v, t);
+    U_apply(P.Rt[0], t, t6);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) o[r] -= t6[r];
+  };
+  auto Gy = [&](const double* yy, double* o) {
+    o[0] = -yy[2]; o[1] = -sec * yy[2]; o[2] = -yy[0]; o[3] = -yy[1]; o[4] = -yy[2];
+    o[5] = 0.0; o[6] = -yy[0]; o[7] = -yy[1]; o[8] = -yy[2];
+  };
+  auto GTz = [&](const double* z, double* o) {
+    o[0] = -(z[2] + z[6]);
+    o[1] = -(z[3] + z[7]);
+    o[2] = -(z[0] + sec * z[1] + z[4] + z[8]);
+  };
+  const double mfz = P.min_fz, mxf = P.max_f;
+  // primal residual of cone block k at the current iterate: G y + s - h
+  double sk[NB][9], zk[NB][9], sl[NROW], zl[NROW];
+  auto rzk_of = [&](int k, double* o) {
+    Gy(y[k], o);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) o[j] += sk[k][j];
+    o[0] += mfz;
+    o[5] -= mxf;
+  };
+  auto compute_u = [&](double* uo) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) uo[r] = (MODE == MODE_CENT) ? 0.0 : w[r];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      double t[6];
+      U_apply(P.Rt[k], y[k], t);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) uo[r] += t[r];
+    }
+  };
+
+  // ---------------- initial point
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) y[k][c] = P.y0[k][c];
+    double g[9];
+    Gy(y[k], g);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) sk[k][j] = -g[j];
+    sk[k][0] -= mfz;
+    sk[k][5] += mxf;
+    // shift into the interior if the guess is not strictly feasible
+    double m1 = sk[k][0], m2 = sk[k][1] - sqrt(sk[k][2] * sk[k][2] + sk[k][3] * sk[k][3] + sk[k][4] * sk[k][4]);
+    double m3 = sk[k][5] - sqrt(sk[k][6] * sk[k][6] + sk[k][7] * sk[k][7] + sk[k][8] * sk[k][8]);
+    double mn = fmin(m1, fmin(m2, m3));
+    if (mn < 1e-3) { sk[k][0] += 1.0 - mn; sk[k][1] += 1.0 - mn; sk[k][5] += 1.0 - mn; }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) zk[k][j] = 0.0;
+    zk[k][0] = 1.0; zk[k][1] = 1.0; zk[k][5] = 1.0;
+  }
+#pragma unroll
+  for (int l = 0; l < NROW; ++l) zl[l] = act(l);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) w[r] = 0.0;
+  if (MODE == MODE_CADMM) {
+    // consistent free aggregate: (rho I + K C) w = rho atil - K (C U y + cu - A' zl)
+    double uy[6], cuy[6], az[6], rhs[6], Kt[6];
+    compute_u(uy);  // w = 0 here
+    spmv6(Cp(), uy, cuy);
+    rows_adj(zl, az);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) cuy[r] += cup()[r] - az[r];
+    Kmul(cuy, Kt);
+    double A[6][6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      double col[6], kc[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) col[r] = Cp()[sp6(r, c)];
+      Kmul(col, kc);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) A[r][c] = kc[r] + (r == c ? P.rho : 0.0);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) rhs[r] = P.rho * P.atil[r] - Kt[r];
+    int piv[6];
+    if (!lu6(A, piv)) return out;
+    lu6_solve(A, piv, rhs);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) w[r] = rhs[r];
+  }
+  {
+    double u[6], dv[3], dw[3];
+    compute_u(u);
+    lin(u, dv, dw);
+#pragma unroll
+    for (int l = 0; l < NROW; ++l) sl[l] = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
+  }
+
+  // scales for the relative stopping rule
+  double nh = 1.0 + fmax(mfz, mxf), nq = 1.0;
+#pragma unroll
+  for (int l = 0; l < NROW; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
+#pragma unroll
+  for (int k = 0; k < NB; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) nq = fmax(nq, 1.0 + fabs(P.q[k][c]));
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
+
+  double best_merit = 1e300, best_y[NB][3], best_w[6], best_pi[6], best_u[6];
+  const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
+
+  for (int it = 0;; ++it) {
+    // ------------- residuals
+    double u[6], dv[3], dw[3];
+    compute_u(u);
+    lin(u, dv, dw);
+    double rk[NB][3], Rf[6];
+    double dres = 0.0, pres = 0.0, gap = 0.0;
+    {
+      double pi[6], az[6];
+      spmv6(Cp(), u, pi);
+      rows_adj(zl, az);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) pi[r] += cup()[r] - az[r];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double ut[3], gz[3];
+        Ut_apply(P.Rt[k], pi, ut);
+        GTz(zk[k], gz);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          rk[k][c] = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
+          dres = fmax(dres, fabs(rk[k][c]));
+        }
+      }
+      if (MODE == MODE_CADMM) {
+        double kp[6];
+        Kmul(pi, kp);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) Rf[r] = P.rho * (w[r] - P.atil[r]) + kp[r];
+      } else if (MODE == MODE_DD) {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) Rf[r] = pi[r] + P.cw[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) Rf[r] = 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) dres = fmax(dres, fabs(Rf[r]));
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double rz[9];
+        rzk_of(k, rz);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          pres = fmax(pres, fabs(rz[j]));
+          gap += sk[k][j] * zk[k][j];
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) {
+        pres = fmax(pres, fabs(sl[l] - (rowdot(l, dv, dw) + rb(l))));
+        gap += sl[l] * zl[l];
+      }
+      out.iters = it;
+      if (!(dres == dres) || !(pres == pres) || !(gap == gap)) {  // NaN
+        out.status = ST_FAILED;
+        break;
+      }
+      double merit = fmax(fmax(pres / nh, dres / nq), gap);
+      if (pres < tol * nh && dres < tol * nq && gap < 10.0 * tol) {
+        out.status = ST_OPTIMAL;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
+        return out;
+      }
+      if (merit < best_merit) {
+        best_merit = merit;
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) best_y[k][c] = y[k][c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) { best_w[r] = w[r]; best_pi[r] = pi[r]; best_u[r] = u[r]; }
+      } else if (merit > 1e3 * best_merit || it >= max_iter) {
+        break;
+      }
+      if (it >= max_iter) break;
+    }
+
+    // ------------- NT scaling of the cone blocks
+    SocScale S1[NB], S2[NB];
+    double id0[NB], lamk[NB][9];
+    bool okc = true;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      id0[k] = sqrt(zk[k][0] * frcp(sk[k][0]));  // 1 / d0, d0 = sqrt(s0 / z0)
+      lamk[k][0] = sqrt(sk[k][0] * zk[k][0]);
+      okc = okc && soc_scaling(sk[k] + 1, zk[k] + 1, S1[k]) && soc_scaling(sk[k] + 5, zk[k] + 5, S2[k]);
+      soc_apply(S1[k], zk[k] + 1, lamk[k] + 1, false);
+      soc_apply(S2[k], zk[k] + 5, lamk[k] + 5, false);
+    }
+    if (!okc) break;
+    auto winv = [&](int k, const double* v, double* o) {  // W_k^-1 v
+      o[0] = v[0] * id0[k];
+      soc_apply(S1[k], v + 1, o + 1, true);
+      soc_apply(S2[k], v + 5, o + 5, true);
+    };
+    // Gs = W^-1 G applied to a 3-vector / its transpose applied to a 9-vector
+    auto gs_mul = [&](int k, const double* v, double* o) {
+      double g[9];
+      Gy(v, g);
+      winv(k, g, o);
+    };
+    auto gs_tmul = [&](int k, const double* t, double* o) {
+      double g[9];
+      winv(k, t, g);
+      GTz(g, o);
+    };
+    // D_k = kappa I + Gs'Gs (packed) and its inverse
+    double Dinv[NB][6];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      double gc[3][9];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        double e[3] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0};
+        gs_mul(k, e, gc[c]);
+      }
+      double D[6];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = r; c < 3; ++c) {
+          double s = (r == c) ? kap : 0.0;
+#pragma unroll
+          for (int j = 0; j < 9; ++j) s += gc[r][j] * gc[c][j];
+          D[sp3(r, c)] = s;
+        }
+      okc = okc && inv3_spd(D, Dinv[k]);
+    }
+    if (!okc) break;
+    // reciprocal slacks of the rows
+    double isl[NROW];
+#pragma unroll
+    for (int l = 0; l < NROW; ++l) isl[l] = frcp(sl[l]);
+    // M (packed) and, for CADMM / CENT, the LU factors of (I + M T); DD: the Cholesky factor of M
+    // parked in LU.  (Forming N = (I + M T)^-1 M explicitly would save registers but loses the
+    // accuracy the refinement needs once active rows make M huge.)
+    double Mm[21], LU[6][6];
+    int piv[6];
+    {
+      // M = C + sum_l (z/s) a_l a_l' (u-space, packed), assembled in (dvl, dwl) coordinates
+      {
+        double Xv[6] = {0, 0, 0, 0, 0, 0}, Xw[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int l = 0; l < NROW; ++l) {
+          const double wgt = zl[l] * isl[l];
+          double* X = l < NWROW ? Xw : Xv;
+          const double a0 = ra(l, 0), a1 = ra(l, 1), a2 = ra(l, 2);
+          X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
+          X[3] += wgt * a1 * a1; X[4] += wgt * a1 * a2; X[5] += wgt * a2 * a2;
+        }
+        // Av = [im I, Bv];  Av' Xv Av = [[im^2 Xv, im Xv Bv], [., Bv' Xv Bv]];  Aw = [0, JTi]
+        const QPShared& S = sh.get();
+        double XB[9], XJ[9];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            XB[3 * r + c] = Xv[sp3(r, 0)] * S.Bv[c] + Xv[sp3(r, 1)] * S.Bv[3 + c] + Xv[sp3(r, 2)] * S.Bv[6 + c];
+            XJ[3 * r + c] = Xw[sp3(r, 0)] * S.JTi[c] + Xw[sp3(r, 1)] * S.JTi[3 + c] + Xw[sp3(r, 2)] * S.JTi[6 + c];
+          }
+        const double* C = S.C[var];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if (c >= r) {
+              Mm[sp6(r, c)] = C[sp6(r, c)] + im * im * Xv[sp3(r, c)];
+              double s = C[sp6(3 + r, 3 + c)];
+#pragma unroll
+              for (int k2 = 0; k2 < 3; ++k2) s += S.Bv[3 * k2 + r] * XB[3 * k2 + c] + S.JTi[3 * k2 + r] * XJ[3 * k2 + c];
+              Mm[sp6(3 + r, 3 + c)] = s;
+            }
+            Mm[sp6(r, 3 + c)] = C[sp6(r, 3 + c)] + im * XB[3 * r + c];
+          }
+      }
+      if (MODE == MODE_DD) {
+        double Lp[21];
+        if (!chol6(Mm, Lp)) break;
+#pragma unroll
+        for (int k = 0; k < 21; ++k) LU[k / 6][k % 6] = Lp[k];
+      } else {
+        // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho);  N = (I + M T)^-1 M, symmetrised
+        double T[21];
+        if (MODE == MODE_CADMM) {
+          const double* K = sh.get().K;
+#pragma unroll
+          for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
+          // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
+          double Dm[6] = {Dinv[0][0] - irho, Dinv[0][1], Dinv[0][2], Dinv[0][3] - irho, Dinv[0][4], Dinv[0][5] - irho};
+          add_UDUt(T, P.Rt[0], Dm, 1.0);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 21; ++k) T[k] = 0.0;
+#pragma unroll
+          for (int k = 0; k < NB; ++k) add_UDUt(T, P.Rt[k], Dinv[k], 1.0);
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s += Mm[sp6(r, k)] * T[sp6(k, c)];
+            LU[r][c] = s;
+          }
+        if (!lu6(LU, piv)) break;
+      }
+    }
+
+    // core structured solve of (D + U'MU) dx = b (CADMM/CENT) or its DD analogue
+    auto core = [&](const double bk[NB][3], const double* Rfr, const double* bu, double dy[NB][3], double* dwo,
+                    double* du) {
+      if (MODE == MODE_DD) {
+        double rw[6], Lp[21];
+#pragma unroll
+        for (int k = 0; k < 21; ++k) Lp[k] = LU[k / 6][k % 6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) rw[r] = -Rfr[r] + bu[r];
+        chol6_solve(Lp, rw);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) du[r] = rw[r];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double t[3], v[3];
+          Ut_apply(P.Rt[k], Rfr, t);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[c] = bk[k][c] + t[c];
+          spmv3(Dinv[k], v, dy[k]);
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dwo[r] = du[r];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double t[6];
+          U_apply(P.Rt[k], dy[k], t);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dwo[r] -= t[r];
+        }
+        return;
+      }
+      double bk2[NB][3], yv[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double t[3], v[3], ut[6];
+        Ut_apply(P.Rt[k], bu, t);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) bk2[k][c] = bk[k][c] + t[c];
+        spmv3(Dinv[k], bk2[k], v);
+        U_apply(P.Rt[k], v, ut);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) yv[r] += ut[r];
+      }
+      double kb[6] = {0, 0, 0, 0, 0, 0};
+      if (MODE == MODE_CADMM) {
+        Kmul(bu, kb);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) yv[r] += (-Rfr[r] + kb[r]) * irho;
+      }
+      double tau[6];
+      spmv6(Mm, yv, tau);
+      lu6_solve(LU, piv, tau);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double t[3], v[3];
+        Ut_apply(P.Rt[k], tau, t);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = bk2[k][c] - t[c];
+        spmv3(Dinv[k], v, dy[k]);
+      }
+      if (MODE == MODE_CADMM) {
+        double kt[6];
+        Kmul(tau, kt);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dwo[r] = (-Rfr[r] + kb[r] - kt[r]) * irho;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dwo[r] = 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) du[r] = (MODE == MODE_CADMM) ? dwo[r] : 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double t[6];
+        U_apply(P.Rt[k], dy[k], t);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) du[r] += t[r];
+      }
+    };
+
+    // Newton direction for complementarity targets rsk (cones, scaled) and, for the rows,
+    // rc_l = s_l z_l + cadd_l (cadd = 0 for the predictor).  Outputs: dy, dw, du, scaled dz of the
+    // cones (dzs_k) and lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k); row dz is zw - (z/s) a.lin(du).
+    double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9], zw[NROW];
+    // tks_k = W^-1 rz_k - lam \ rsk
+    auto tks_of = [&](int k, double* t) {
+      double rz[9];
+      rzk_of(k, rz);
+      winv(k, rz, t);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) t[j] -= lrs_k[k][j];
+    };
+    auto newton = [&](const double rsk[NB][9], const double* cadd) {
+      double bk[NB][3], bu[6];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        lrs_k[k][0] = rsk[k][0] * frcp(lamk[k][0]);
+        soc_jdiv(lamk[k] + 1, rsk[k] + 1, lrs_k[k] + 1);
+        soc_jdiv(lamk[k] + 5, rsk[k] + 5, lrs_k[k] + 5);
+        double tks[9], g3[3];
+        tks_of(k, tks);
+        gs_tmul(k, tks, g3);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) bk[k][c] = -rk[k][c] - g3[c];
+      }
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) {
+        const double rzl = sl[l] - (rowdot(l, dv, dw) + rb(l));
+        zw[l] = (zl[l] * rzl - (sl[l] * zl[l] + cadd[l])) * isl[l];
+      }
+      rows_adj(zw, bu);
+      core(bk, Rf, bu, dy, dwv, du);
+      for (int ref = 0; ref < 2; ++ref) {
+        // linearised dual residual of the full system at (dy, dw); refine
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double tks[9], g9[9];
+          tks_of(k, tks);
+          gs_mul(k, dy[k], g9);
+#pragma unroll
+          for (int j = 0; j < 9; ++j) dzs_k[k][j] = tks[j] + g9[j];
+        }
+        double ddv[3], ddw[3], dzl[NROW], dpi[6], adz[6];
+        lin(du, ddv, ddw);
+#pragma unroll
+        for (int l = 0; l < NROW; ++l) dzl[l] = zw[l] - zl[l] * isl[l] * rowdot(l, ddv, ddw);
+        spmv6(Cp(), du, dpi);
+        rows_adj(dzl, adz);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dpi[r] -= adz[r];
+        double ek[NB][3], ef[6];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double ut[3], g3[3];
+          Ut_apply(P.Rt[k], dpi, ut);
+          gs_tmul(k, dzs_k[k], g3);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) ek[k][c] = -(kap * dy[k][c] + ut[c] + g3[c] + rk[k][c]);
+        }
+        if (MODE == MODE_CADMM) {
+          double kp[6];
+          Kmul(dpi, kp);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) ef[r] = P.rho * dwv[r] + kp[r] + Rf[r];
+        } else if (MODE == MODE_DD) {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) ef[r] = dpi[r] + Rf[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) ef[r] = 0.0;
+        }
+        double zero6[6] = {0, 0, 0, 0, 0, 0}, cy[NB][3], cw6[6], cu6[6];
+        core(ek, ef, zero6, cy, cw6, cu6);
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) dy[k][c] += cy[k][c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) { dwv[r] += cw6[r]; du[r] += cu6[r]; }
+      }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double tks[9], g9[9];
+        tks_of(k, tks);
+        gs_mul(k, dy[k], g9);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) dzs_k[k][j] = tks[j] + g9[j];
+      }
+    };
+    // row directions of the current Newton solution
+    auto row_dirs = [&](int l, const double* ddv, const double* ddw, double& ds, double& dz) {
+      const double a = rowdot(l, ddv, ddw);
+      ds = -(sl[l] - (rowdot(l, dv, dw) + rb(l))) + a;
+      dz = zw[l] - zl[l] * isl[l] * a;
+    };
+    auto step_len = [&]() {
+      double a = 1e300;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double dss[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) dss[j] = -lrs_k[k][j] - dzs_k[k][j];
+        if (dss[0] < 0) a = fmin(a, -lamk[k][0] * frcp(dss[0]));
+        if (dzs_k[k][0] < 0) a = fmin(a, -lamk[k][0] * frcp(dzs_k[k][0]));
+        a = fmin(a, soc_step(lamk[k] + 1, dss + 1));
+        a = fmin(a, soc_step(lamk[k] + 1, dzs_k[k] + 1));
+        a = fmin(a, soc_step(lamk[k] + 5, dss + 5));
+        a = fmin(a, soc_step(lamk[k] + 5, dzs_k[k] + 5));
+      }
+      double ddv[3], ddw[3];
+      lin(du, ddv, ddw);
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) {
+        double ds, dz;
+        row_dirs(l, ddv, ddw, ds, dz);
+        if (ds < 0) a = fmin(a, -sl[l] * frcp(ds));
+        if (dz < 0) a = fmin(a, -zl[l] * frcp(dz));
+      }
+      return a;
+    };
+    auto gap_at = [&](double al) {
+      double g = 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          double dss = -lrs_k[k][j] - dzs_k[k][j];
+          g += (lamk[k][j] + al * dss) * (lamk[k][j] + al * dzs_k[k][j]);
+        }
+      double ddv[3], ddw[3];
+      lin(du, ddv, ddw);
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) {
+        double ds, dz;
+        row_dirs(l, ddv, ddw, ds, dz);
+        g += (sl[l] + al * ds) * (zl[l] + al * dz);
+      }
+      return g;
+    };
+
+    // predictor
+    {
+      double rsk[NB][9], cadd[NROW];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        rsk[k][0] = lamk[k][0] * lamk[k][0];
+        soc_jprod(lamk[k] + 1, lamk[k] + 1, rsk[k] + 1);
+        soc_jprod(lamk[k] + 5, lamk[k] + 5, rsk[k] + 5);
+      }
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) cadd[l] = 0.0;
+      newton(rsk, cadd);
+    }
+    {
+      const double aaff = fmin(1.0, step_len());
+      const double gaff = gap_at(aaff);
+      double sig = gaff / gap;
+      sig = fmax(0.0, fmin(1.0, sig * sig * sig));
+      const double sigmu = sig * gap * ideg;
+      // corrector: rs = lam o lam + dss_aff o dzs_aff - sig mu e
+      double rsk[NB][9], cadd[NROW];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double dss[9], c1[4], c2[4];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) dss[j] = -lrs_k[k][j] - dzs_k[k][j];
+        rsk[k][0] = lamk[k][0] * lamk[k][0] + dss[0] * dzs_k[k][0] - sigmu;
+        soc_jprod(lamk[k] + 1, lamk[k] + 1, rsk[k] + 1);
+        soc_jprod(lamk[k] + 5, lamk[k] + 5, rsk[k] + 5);
+        soc_jprod(dss + 1, dzs_k[k] + 1, c1);
+        soc_jprod(dss + 5, dzs_k[k] + 5, c2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { rsk[k][1 + j] += c1[j]; rsk[k][5 + j] += c2[j]; }
+        rsk[k][1] -= sigmu;
+        rsk[k][5] -= sigmu;
+      }
+      {
+        double ddv[3], ddw[3];
+        lin(du, ddv, ddw);
+#pragma unroll
+        for (int l = 0; l < NROW; ++l) {
+          double ds, dz;
+          row_dirs(l, ddv, ddw, ds, dz);
+          cadd[l] = act(l) * (ds * dz - sigmu);
+        }
+      }
+      newton(rsk, cadd);
+    }
+    double alpha = fmin(1.0, 0.99 * step_len());
+    // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
+    // backtrack until the complementarity gap decreases
+    const bool feasible = pres < 1e-8 * nh && dres < 1e-8 * nq;
+    for (int bt = 0; feasible && bt < 8; ++bt) {
+      if (gap_at(alpha) <= gap * (1.0 - 0.01 * alpha)) break;
+      alpha *= 0.5;
+    }
+    // update.  ds from the primal equation (keeps G y + s = h exact), dz = W^-1 dzs.
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      double g[9], dz[9], rz[9];
+      Gy(dy[k], g);
+      winv(k, dzs_k[k], dz);
+      rzk_of(k, rz);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        sk[k][j] += alpha * (-rz[j] - g[j]);
+        zk[k][j] += alpha * dz[j];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) y[k][c] += alpha * dy[k][c];
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) w[r] += alpha * dwv[r];
+    {
+      double ddv[3], ddw[3];
+      lin(du, ddv, ddw);
+#pragma unroll
+      for (int l = 0; l < NROW; ++l) {
+        double ds, dz;
+        row_dirs(l, ddv, ddw, ds, dz);
+        sl[l] += alpha * ds;
+        zl[l] += alpha * dz;
+      }
+    }
+  }
+  // not converged to tol: return the best iterate seen; "optimal" if within 100 tol (Clarabel's
+  // reduced-accuracy band), otherwise inaccurate (the reference holds its previous solution).
+  if (best_merit < 1e300) {
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) y[k][c] = best_y[k][c];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) { w[r] = best_w[r]; out.pi[r] = best_pi[r]; out.u[r] = best_u[r]; }
+    out.status = best_merit < 1e2 * tol ? ST_OPTIMAL : ST_INACCURATE;
+  }
+  return out;
+}
+
+
+}  // namespace dat

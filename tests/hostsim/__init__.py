@@ -12,7 +12,7 @@ CORE = os.path.join(os.path.dirname(os.path.dirname(HERE)), "distributed_aerial_
 
 
 def build(force=False):
-    deps = [SRC] + [os.path.join(CORE, f) for f in ("dat_core.hpp", "dat_layout.h")]
+    deps = [SRC] + [os.path.join(CORE, f) for f in ("dat_core.hpp", "dat_qp.hpp", "dat_layout.h")]
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(d) for d in deps):
         subprocess.check_call(["hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
                                SRC, "-o", LIB])

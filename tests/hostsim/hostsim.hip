@@ -4,7 +4,7 @@
 // the product package): it runs the exact __host__ __device__ code of one GPU lane on the CPU so
 // the reduced-QP algebra, the env rows and the rollout can be checked against the oracle in the
 // dev container, which has no GPU.  The product path has no CPU fallback.
-#include "../../distributed_aerial_transportation_amd/csrc/dat_core.hpp"
+#include "../../distributed_aerial_transportation_amd/csrc/dat_qp.hpp"
 
 using namespace dat;
 
@@ -12,35 +12,92 @@ using namespace dat;
 #define HS_TOL 1e-10
 #endif
 
+namespace {
+// compacted (nenv x 3, nenv) env rows -> slot arrays + mask
+void env_slots(const double* env_lhs, const double* env_rhs, int nenv, double lhs[DAT_NENV][3], double rhs[DAT_NENV],
+               unsigned* mask) {
+  *mask = 0u;
+  for (int j = 0; j < DAT_NENV; ++j) {
+    lhs[j][0] = lhs[j][1] = lhs[j][2] = 0.0;
+    rhs[j] = 0.0;
+    if (j < nenv) {
+      for (int c = 0; c < 3; ++c) lhs[j][c] = env_lhs[3 * j + c];
+      rhs[j] = env_rhs[j];
+      *mask |= 1u << j;
+    }
+  }
+}
+template <int NB>
+int cent_nb(const double* prm, const double* st, const double* acc, const double* env_lhs, const double* env_rhs,
+            int nenv, double* f_out, int* iters) {
+  QPShared S;
+  build_shared(S, prm, NB, st, acc, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
+  QPLane<NB> P;
+  lane_cent(P, prm, NB, st);
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  unsigned mask;
+  env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
+  EnvRows E;
+  set_env_rows(P, E, S, mask, lhs, rhs);
+  double y[NB][3], w[6];
+  IPMOut o = ipm_solve<MODE_CENT, NB>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
+  for (int k = 0; k < NB; ++k)
+    for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
+  *iters = o.iters;
+  return o.status;
+}
+
+}  // namespace
+
 extern "C" {
 
 int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                 const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
                 double* f_out, int* iters) {
+  if (nenv > DAT_NENV) return -1;
   double Rt_all[16 * 9];
   const double* Rl = st + DAT_S_RL(n);
   for (int j = 0; j < n; ++j) make_Rt(prm + DAT_P_RCOM(n) + 3 * j, Rl, Rt_all + 9 * j);
-  QP<1> P;
-  build_cadmm_static(P, prm, n, st, acc, i, Rt_all);
-  add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
-  build_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
+  QPShared S;
+  build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+  QPLane<1> P;
+  lane_cadmm_static(P, prm, n, i, Rt_all + 9 * i);
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  unsigned mask;
+  env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
+  EnvRows E;
+  set_env_rows(P, E, S, mask, lhs, rhs);
+  lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_CADMM, 1>(P, y, w, 50, HS_TOL);
-  cadmm_materialize(P, n, i, Rt_all, lam, fbar, y[0], o.pi, f_out);
+  IPMOut o = ipm_solve<MODE_CADMM, 1>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
+  for (int j = 0; j < n; ++j) {
+    if (j == i) {
+      for (int c = 0; c < 3; ++c) f_out[3 * j + c] = y[0][c];
+    } else {
+      cadmm_free_block(Rt_all + 9 * j, lam + 3 * j, fbar + 3 * j, o.pi, rho, f_out + 3 * j);
+    }
+  }
   *iters = o.iters;
   return o.status;
 }
 
 int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
              const double* env_rhs, int nenv, int i, const double* c9, double* x_out, int* iters) {
+  if (nenv > DAT_NENV) return -1;
   double Rt[9];
   make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), Rt);
-  QP<1> P;
-  build_dd_static(P, prm, n, st, acc, i, Rt);
+  QPShared S;
+  build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
+  QPLane<1> P;
+  lane_dd_static(P, prm, n, i, Rt);
   set_dd_price(P, prm, n, i, c9);
-  add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  unsigned mask;
+  env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
+  EnvRows E;
+  set_env_rows(P, E, S, mask, lhs, rhs);
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_DD, 1>(P, y, w, 50, HS_TOL);
+  IPMOut o = ipm_solve<MODE_DD, 1>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
   for (int c = 0; c < 3; ++c) x_out[c] = y[0][c];
   for (int c = 0; c < 6; ++c) x_out[3 + c] = w[c];
   *iters = o.iters;
@@ -49,39 +106,27 @@ int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, cons
 
 int hs_qp_cent(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                const double* env_rhs, int nenv, double* f_out, int* iters) {
-  if (n != 3 && n != 6) return -1;
-  int status;
-  if (n == 3) {
-    QP<3> P;
-    build_cent(P, prm, n, st, acc);
-    add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
-    double y[3][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, 3>(P, y, w, 50, HS_TOL);
-    for (int k = 0; k < 3; ++k)
-      for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
-    *iters = o.iters;
-    status = o.status;
-  } else {
-    QP<6> P;
-    build_cent(P, prm, n, st, acc);
-    add_env_rows(P, nenv, (const double(*)[3])env_lhs, env_rhs);
-    double y[6][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, 6>(P, y, w, 50, HS_TOL);
-    for (int k = 0; k < 6; ++k)
-      for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
-    *iters = o.iters;
-    status = o.status;
-  }
-  return status;
+  if (nenv > DAT_NENV) return -1;
+  if (n == 3) return cent_nb<3>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
+  if (n == 6) return cent_nb<6>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
+  return -1;
 }
 
 int hs_env_rows(const double* prm, int n, const double* st, const double* trees, int ntree, int agent,
                 double alpha, double* lhs, double* rhs, int* collision, double* min_dist) {
-  int nrow = 0;
-  EnvOut e = env_rows(prm, n, st, trees, ntree, agent, alpha, &nrow, (double(*)[3])lhs, rhs);
+  double L[DAT_NENV][3], R[DAT_NENV];
+  unsigned mask;
+  EnvOut e = env_rows(prm, n, st, trees, ntree, agent, alpha, &mask, L, R);
   *collision = e.collision;
   *min_dist = e.min_env_dist;
-  return nrow;
+  int k = 0;
+  for (int j = 0; j < DAT_NENV; ++j) {
+    if (!((mask >> j) & 1u)) continue;
+    for (int c = 0; c < 3; ++c) lhs[3 * k + c] = L[j][c];
+    rhs[k] = R[j];
+    ++k;
+  }
+  return k;
 }
 
 void hs_sim_step(const double* prm, int n, double* st, int* counter, const double* fdes, double dt) {
