@@ -65,6 +65,7 @@ struct KArgs {
   double *cf, *cfbar, *clam;                 // C-ADMM warm state
   double *dlamF, *dlamM, *dprev, *dHinv;      // DD state
   double* pf;                                 // centralized previous solution
+  double* best;                               // lane-private best-iterate records of the IPM
   int* iters;
   int* qstatus;
   double* mind;
@@ -72,6 +73,12 @@ struct KArgs {
   double* err;
   unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations
 };
+
+// wave-uniform maximum (every lane of the wavefront must execute it)
+__device__ inline int wave_max(int v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
 
 __device__ inline const double* prm_of(const KArgs& a, int sc) { return a.params + (a.ppp ? (size_t)sc * a.P : 0); }
 
@@ -88,31 +95,35 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 // ------------------------------------------------------------------------------------------------
 // C-ADMM
 // ------------------------------------------------------------------------------------------------
-// LDS layout of one 64-lane block (G = floor(64/n) scenarios):
-//   fx   NT x 3n   agent copies f^(i)            fbar G x 3n   consensus mean
-//   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x 8   per-lane exchange slots
-//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)   env 64 x EnvRows   done G ints
+// LDS layout of one 64-lane block (G = floor(64/n) scenarios).  Per-lane records use an odd
+// stride in doubles so that the 32 lanes of a ds_read_b64 group fall on distinct bank pairs.
+//   fx   NT x FXS  agent copies f^(i) (FXS = 3n rounded up to odd)    fbar G x 3n  consensus mean
+//   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x RDS (9)  per-lane exchange slots
+//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)
+//   env  EnvLds image (structure of arrays over the 64 lanes)        done G ints
+constexpr int RDS = 9;
+__host__ __device__ inline int fx_stride(int n) { return (3 * n) | 1; }
 struct CadmmLds {
   double *fx, *fbar, *Rt, *red;
   QPShared* sh;
-  EnvRows* env;
+  double* env;
   int* done;
 };
 __host__ __device__ inline size_t cadmm_lds_bytes(int n) {
   const int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * 3 * n + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * 8) +
-         sizeof(QPShared) * (size_t)G + sizeof(EnvRows) * 64 + sizeof(int) * 64;
+  return sizeof(double) * ((size_t)NT * fx_stride(n) + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * RDS) +
+         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES + sizeof(int) * 64;
 }
 __device__ inline CadmmLds cadmm_carve(double* smem, int n) {
   const int G = 64 / n, NT = G * n;
   CadmmLds L;
   L.fx = smem;
-  L.fbar = L.fx + NT * 3 * n;
+  L.fbar = L.fx + NT * fx_stride(n);
   L.Rt = L.fbar + G * 3 * n;
   L.red = L.Rt + G * 9 * n;
-  L.sh = (QPShared*)(L.red + 64 * 8);
-  L.env = (EnvRows*)(L.sh + G);
-  L.done = (int*)(L.env + 64);
+  L.sh = (QPShared*)(L.red + 64 * RDS);
+  L.env = (double*)(L.sh + G);
+  L.done = (int*)(L.env + ENV_LDS_DOUBLES);
   return L;
 }
 
@@ -125,10 +136,11 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   const int sc = blockIdx.x * G + ls;
   const bool valid = (lane < NT) && (sc < a.B);
   CadmmLds L = cadmm_carve(smem, n);
-  double* myf = L.fx + lane * N3;
+  const int FXS = fx_stride(n);
+  double* myf = L.fx + lane * FXS;
   double* fb = L.fbar + ls * N3;
   double* rts = L.Rt + ls * 9 * n;
-  double* myred = L.red + lane * 8;
+  double* myred = L.red + lane * RDS;
   QPShared& S = L.sh[ls < G ? ls : 0];
 
   QPLane<1> P;
@@ -154,26 +166,34 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     L.done[ls] = 1;
   }
   __syncthreads();
+  int nr = NBASE;
   if (valid) {
     const double* st = a.state + (size_t)sc * a.S;
-    lane_cadmm_static(P, prm, n, i, rts + 9 * i);
+    lane_cadmm_static(P, prm, i);
     const double* trees;
     int nt;
     unsigned emask;
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
     env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
-    set_env_rows(P, L.env[lane], S, emask, lhs, rhs);
+    EnvRows E;
+    set_env_rows(P, E, S, emask, lhs, rhs);
+    env_to_lds(L.env, lane, E);
+    nr = rows_needed(P.emask);
   }
+  nr = wave_max(nr);
   const LdsRef<QPShared> shr{L.sh, ls < G ? ls : 0};
-  const LdsRef<EnvRows> err{L.env, lane};
+  const EnvLds err{L.env, lane};
+  const RtLds rtr{L.Rt, (ls < G ? ls : 0) * 9 * n + 9 * i};
+  double* bst = a.best + (valid ? ((size_t)sc * n + i) * best_size(1) : 0);
+  const double* y0 = valid ? prm + DAT_P_FEQ(n) + 3 * i : nullptr;
   double rho = a.rho0;
   for (;;) {
     const bool active = valid && !L.done[ls];
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_CADMM, 1>(shr, err, P, y, w, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
       ++my_qp;
       qstat = o.status;
@@ -196,7 +216,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
       // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
       for (int c = 0; c < 3; ++c) {
         double s = 0.0;
-        for (int k = 0; k < n; ++k) s += L.fx[(ls * n + k) * N3 + 3 * i + c];
+        for (int k = 0; k < n; ++k) s += L.fx[(ls * n + k) * FXS + 3 * i + c];
         myred[c] = s / n;
       }
     }
@@ -226,7 +246,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
         // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
         for (int k = 0; k < n; ++k) {
           if (k == i) continue;
-          const double* fk = L.fx + (ls * n + k) * N3 + 3 * k;  // f_app_k = agent k's own block
+          const double* fk = L.fx + (ls * n + k) * FXS + 3 * k;  // f_app_k = agent k's own block
           double m3[3];
           mv3(rts + 9 * k, fk, m3);
           for (int c = 0; c < 3; ++c) { F[c] -= fk[c]; M[c] -= m3[c]; }
@@ -237,26 +257,26 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     __syncthreads();
     if (active && i == 0) {
       double res = 0.0;
-      const double* rg = L.red + (ls * n) * 8;
+      const double* rg = L.red + (ls * n) * RDS;
       if (a.use_total_res) {
-        for (int k = 0; k < n; ++k) res = fmax(res, rg[8 * k + 6]);
+        for (int k = 0; k < n; ++k) res = fmax(res, rg[RDS * k + 6]);
       } else {
         for (int r = 0; r < 3; ++r) {
           double sF = 0.0, sM = 0.0;
           for (int k = 0; k < n; ++k) {
-            sF += fabs(rg[8 * k + r]);
-            sM += fabs(rg[8 * k + 3 + r]);
+            sF += fabs(rg[RDS * k + r]);
+            sM += fabs(rg[RDS * k + 3 + r]);
           }
           res = fmax(res, fmax(sF, sM));
         }
       }
       bool stop = (res < a.res_tol) || (iter > a.max_iter);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
-      L.red[(ls * n) * 8 + 7] = stop ? 1.0 : 0.0;
+      L.red[(ls * n) * RDS + 7] = stop ? 1.0 : 0.0;
     }
     __syncthreads();
     if (active) {
-      bool stop = L.red[(ls * n) * 8 + 7] != 0.0;
+      bool stop = L.red[(ls * n) * RDS + 7] != 0.0;
       if (!stop) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
       }
@@ -264,7 +284,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     __syncthreads();
     int any = 0;
     if (active && i == 0) {
-      bool stop = L.red[(ls * n) * 8 + 7] != 0.0;
+      bool stop = L.red[(ls * n) * RDS + 7] != 0.0;
       L.done[ls] = stop ? 1 : 0;
       any = stop ? 0 : 1;
     }
@@ -287,8 +307,8 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     int coll = 0;
     double md = prm[DAT_P_VISR];
     for (int k = 0; k < n; ++k) {
-      coll |= L.red[(ls * n + k) * 8] != 0.0;
-      md = fmin(md, L.red[(ls * n + k) * 8 + 1]);
+      coll |= L.red[(ls * n + k) * RDS] != 0.0;
+      md = fmin(md, L.red[(ls * n + k) * RDS + 1]);
     }
     a.col[sc] = (unsigned char)coll;
     a.mind[sc] = md;
@@ -446,6 +466,7 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 // DD step
 // ------------------------------------------------------------------------------------------------
+constexpr int DD_ES = 7, DD_RS = 5;
 __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n, N6 = 6 * n;
@@ -457,11 +478,11 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* X = smem;                 // NT x 9   (f_i, F_i, M_i)
   double* lamF = X + NT * 9;        // G x 3n
   double* lamM = lamF + G * N3;     // G x 3n
-  double* E = lamM + G * N3;        // NT x 6   consensus error
-  double* Rts = E + NT * 6;         // G x 9n
-  double* red = Rts + G * 9 * n;    // 64 x 4
-  QPShared* shs = (QPShared*)(red + 64 * 4);  // G
-  EnvRows* envs = (EnvRows*)(shs + G);        // 64
+  double* E = lamM + G * N3;        // NT x ES  consensus error (ES = 7: odd stride, no bank conflicts)
+  double* Rts = E + NT * DD_ES;     // G x 9n
+  double* red = Rts + G * 9 * n;    // 64 x DD_RS
+  QPShared* shs = (QPShared*)(red + 64 * DD_RS);  // G
+  double* envs = (double*)(shs + G);              // EnvLds image
   QPShared& S = shs[ls < G ? ls : 0];
   double* myX = X + lane * 9;
   double* lF = lamF + ls * N3;
@@ -487,24 +508,32 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
     if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
   }
-  if (lane < 64) red[lane * 4 + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
+  if (lane < 64) red[lane * DD_RS + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
   __syncthreads();
+  int nr = NBASE;
   if (valid) {
     const double* st = a.state + (size_t)sc * a.S;
-    lane_dd_static(P, prm, n, i, rts + 9 * i);
+    lane_dd_static(P, prm, i);
     const double* trees;
     int nt;
     unsigned emask;
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
     env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
-    set_env_rows(P, envs[lane], S, emask, lhs, rhs);
+    EnvRows Ev;
+    set_env_rows(P, Ev, S, emask, lhs, rhs);
+    env_to_lds(envs, lane, Ev);
+    nr = rows_needed(P.emask);
   }
+  nr = wave_max(nr);
   const LdsRef<QPShared> shr{shs, ls < G ? ls : 0};
-  const LdsRef<EnvRows> err{envs, lane};
+  const EnvLds err{envs, lane};
+  const RtLds rtr{Rts, (ls < G ? ls : 0) * 9 * n + 9 * i};
+  double* bst = a.best + (valid ? ((size_t)sc * n + i) * best_size(1) : 0);
+  const double* y0 = valid ? prm + DAT_P_FEQ(n) + 3 * i : nullptr;
   const double* Rl = valid ? a.state + (size_t)sc * a.S + DAT_S_RL(n) : nullptr;
   for (;;) {
-    const bool active = valid && red[(ls * n) * 4 + 3] == 0.0;
+    const bool active = valid && red[(ls * n) * DD_RS + 3] == 0.0;
     if (active) {
       // prices (control/rqp_dd.py:718-722)
       double sF[3] = {0, 0, 0}, sM[3] = {0, 0, 0};
@@ -521,7 +550,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       }
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_DD, 1>(shr, err, P, y, w, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
       ++my_qp;
       qstat = o.status;
@@ -553,8 +582,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int c = 0; c < 3; ++c) { sf[c] += fk[c]; sm[c] += m3[c]; }
       }
       for (int c = 0; c < 3; ++c) {
-        E[lane * 6 + c] = myX[3 + c] - sf[c];
-        E[lane * 6 + 3 + c] = myX[6 + c] - sm[c];
+        E[lane * DD_ES + c] = myX[3 + c] - sf[c];
+        E[lane * DD_ES + 3 + c] = myX[6 + c] - sm[c];
       }
     }
     __syncthreads();
@@ -562,25 +591,25 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       double res = 0.0;
       for (int r = 0; r < 6; ++r) {
         double s = 0.0;
-        for (int k = 0; k < n; ++k) s += fabs(E[(ls * n + k) * 6 + r]);
+        for (int k = 0; k < n; ++k) s += fabs(E[(ls * n + k) * DD_ES + r]);
         res = fmax(res, s);
       }
       bool stop = (res < a.res_tol) || (iter > a.max_iter);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
-      red[(ls * n) * 4 + 2] = stop ? 1.0 : 0.0;
+      red[(ls * n) * DD_RS + 2] = stop ? 1.0 : 0.0;
     }
     __syncthreads();
-    if (active && red[(ls * n) * 4 + 2] == 0.0) {
+    if (active && red[(ls * n) * DD_RS + 2] == 0.0) {
       // dual ascent: lambda += H^-1 (A x)   (control/rqp_dd.py:678-693); rows 6i..6i+5
       const double* Hi = a.dHinv + (size_t)sc * N6 * N6;
       double stp[6];
       for (int r = 0; r < 6; ++r) {
         const double* row = Hi + (size_t)(6 * i + r) * N6;
         double s = 0.0;
-        for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * 6 + c % 6];
+        for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * DD_ES + c % 6];
         stp[r] = s;
       }
-      red[lane * 4 + 0] = 0.0;
+      red[lane * DD_RS + 0] = 0.0;
       for (int c = 0; c < 3; ++c) {
         lF[3 * i + c] += stp[c];
         lM[3 * i + c] += stp[3 + c];
@@ -589,8 +618,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     __syncthreads();
     int any = 0;
     if (active && i == 0) {
-      bool stop = red[(ls * n) * 4 + 2] != 0.0;
-      red[(ls * n) * 4 + 3] = stop ? 1.0 : 0.0;
+      bool stop = red[(ls * n) * DD_RS + 2] != 0.0;
+      red[(ls * n) * DD_RS + 3] = stop ? 1.0 : 0.0;
       any = stop ? 0 : 1;
     }
     if (!__syncthreads_or(any)) break;
@@ -603,8 +632,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     }
     for (int c = 0; c < 9; ++c) a.dprev[((size_t)sc * n + i) * 9 + c] = prev[c];
     a.qstatus[(size_t)sc * n + i] = qstat;
-    red[lane * 4 + 0] = env.collision ? 1.0 : 0.0;
-    red[lane * 4 + 1] = env.min_env_dist;
+    red[lane * DD_RS + 0] = env.collision ? 1.0 : 0.0;
+    red[lane * DD_RS + 1] = env.min_env_dist;
   }
   __syncthreads();
   if (valid && i == 0) {
@@ -612,8 +641,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     int coll = 0;
     double md = prm[DAT_P_VISR];
     for (int k = 0; k < n; ++k) {
-      coll |= red[(ls * n + k) * 4] != 0.0;
-      md = fmin(md, red[(ls * n + k) * 4 + 1]);
+      coll |= red[(ls * n + k) * DD_RS] != 0.0;
+      md = fmin(md, red[(ls * n + k) * DD_RS + 1]);
     }
     a.col[sc] = (unsigned char)coll;
     a.mind[sc] = md;
@@ -635,25 +664,37 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
 template <int NB>
 __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = sc < a.B;
+  const int n = NB;
   unsigned long long q = 0, ip = 0;
-  if (sc < a.B) {
-    const int n = NB;
-    const double* prm = prm_of(a, sc);
+  const double* prm = valid ? prm_of(a, sc) : a.params;
+  QPShared S;
+  QPLane<NB> P;
+  double Rt[NB][9];
+  EnvRows E;
+  EnvOut env;
+  env.collision = 0;
+  env.min_env_dist = 0.0;
+  int nr = NBASE;
+  if (valid) {
     const double* st = a.state + (size_t)sc * a.S;
-    QPShared S;
     build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
-    QPLane<NB> P;
-    lane_cent<NB>(P, prm, n, st);
+    lane_cent<NB>(P, prm, n, st, Rt);
     const double* trees;
     int nt;
     unsigned emask;
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    EnvOut env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &emask, lhs, rhs);
-    EnvRows E;
+    env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &emask, lhs, rhs);
     set_env_rows(P, E, S, emask, lhs, rhs);
+    nr = rows_needed(P.emask);
+  }
+  nr = wave_max(nr);
+  if (valid) {
     double y[NB][3], w[6];
-    IPMOut o = ipm_solve<MODE_CENT, NB>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, IPM_MAX_ITER, IPM_TOL);
+    IPMOut o = ipm_solve_rows<MODE_CENT, NB>(nr, PlainRef<QPShared>{&S}, EnvPlain{&E}, RtPtr{&Rt[0][0]}, P,
+                                             prm + DAT_P_FEQ(n), y, w, a.best + (size_t)sc * best_size(NB),
+                                             IPM_MAX_ITER, IPM_TOL);
     q = 1;
     ip = o.iters;
     double* pf = a.pf + (size_t)sc * 3 * n;
@@ -796,6 +837,7 @@ struct dat_handle {
   double *cf = nullptr, *cfbar = nullptr, *clam = nullptr;
   double *dlamF = nullptr, *dlamM = nullptr, *dprev = nullptr, *dHinv = nullptr;
   double* pf = nullptr;
+  double* best = nullptr;
   int *iters = nullptr, *qstatus = nullptr;
   double *mind = nullptr, *err = nullptr;
   unsigned char* col = nullptr;
@@ -858,6 +900,7 @@ KArgs kargs(dat_handle* h) {
   a.dprev = h->dprev;
   a.dHinv = h->dHinv;
   a.pf = h->pf;
+  a.best = h->best;
   a.iters = h->iters;
   a.qstatus = h->qstatus;
   a.mind = h->mind;
@@ -869,8 +912,8 @@ KArgs kargs(dat_handle* h) {
 
 size_t dd_lds(int n) {
   int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * 6 + (size_t)G * 9 * n + 64 * 4) +
-         sizeof(QPShared) * (size_t)G + sizeof(EnvRows) * 64;
+  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * DD_ES + (size_t)G * 9 * n + 64 * DD_RS) +
+         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES;
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
@@ -990,6 +1033,8 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   } else {
     rc |= dalloc(h, &h->pf, B * N3);
   }
+  // lane-private IPM best-iterate records
+  rc |= dalloc(h, &h->best, c.mode == DAT_MODE_CENTRALIZED ? B * (size_t)best_size(c.n) : B * n * (size_t)best_size(1));
   if (rc) {
     std::string m = g_err;
     dat_destroy(h);

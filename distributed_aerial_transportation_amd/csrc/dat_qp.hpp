@@ -4,10 +4,14 @@
 //   QPShared   everything that is the same for all agents of one scenario (u-maps, the packed
 //              u-space Hessians, the base rows, the C-ADMM aggregate K).  The C-ADMM / DD kernels
 //              keep one copy per scenario in LDS; the centralized kernel keeps it in registers.
-//   QPLane     the agent's own data (cone block constants, env rows, linear terms) in registers.
-// Every array the solver touches is indexed with compile-time indices only (rows are fixed slots
-// with an activity mask, loops are unrolled, the LU row exchange is a predicated swap), so
-// nothing is demoted to scratch memory.
+//   EnvRows    the agent's env CBF rows (LDS in the C-ADMM / DD kernels).
+//   Rt         the agent's U-map hat(r_com) Rl' (LDS in the C-ADMM / DD kernels), read through an
+//              accessor at each use.
+//   QPLane     the agent's per-solve scalars and linear terms (registers).
+//   best       the best iterate seen (lane-private global memory: written, read only on failure).
+// Every array the solver keeps in registers is indexed with compile-time indices only (rows are
+// fixed slots with an activity mask, loops are unrolled, the LU row exchange is a predicated
+// swap), so nothing is demoted to scratch memory.
 //
 // u = (S, Mo) in R^6: aggregate force and moment about the CoM in payload axes,
 //   S = sum_j f_j,  Mo = sum_j hat(r_com_j) Rl' f_j      (control/rqp_cadmm.py:376-392)
@@ -17,19 +21,20 @@
 //                                  bv = -g e3 - Rl hat(wl)^2 x_com + Rl hat(x_com) bw
 // Cone block k (an agent's own force f_k in R^3): f_kz >= min_fz, ||f_k|| <= sec f_kz,
 // ||f_k|| <= max_f.  Row slots (affine in (dvl, dwl)):  0 tilt (dwl), 1 |wl| (dwl), 2 |vl| (dvl),
-// 3 .. 3+DAT_NENV-1 env CBFs (dvl).
+// 3 .. 3+DAT_NENV-1 env CBFs (dvl).  Active env rows are compacted to the front of the env
+// slots, so a solve whose rows all fit in NR slots runs the NR-slot instantiation.
 #pragma once
 
 #include "dat_core.hpp"
 
 namespace dat {
 
-#ifndef DAT_IPM_NROW
-#define DAT_IPM_NROW DAT_MAXROW
-#endif
-constexpr int NROW = DAT_IPM_NROW;  // row slots processed by the solver (tools/micro overrides it)
 constexpr int NWROW = 2;          // slots [0, NWROW) act on dwl
 constexpr int NBASE = 3;          // base slots shared by all agents of a scenario
+#ifndef DAT_IPM_NREF
+#define DAT_IPM_NREF 2
+#endif
+constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton solve
 
 struct QPShared {
   double inv_mT, Bv[9], JTi[9], bv[3], bw[3];
@@ -66,19 +71,71 @@ struct LdsRef {
     return base[j];
   }
 };
+// env-row accessors: a(j, c), b(j) of env slot j
+struct EnvPlain {
+  const EnvRows* p;
+  DAT_HD double a(int j, int c) const { return p->a[j][c]; }
+  DAT_HD double b(int j) const { return p->b[j]; }
+};
+// LDS image of the env rows of a 64-lane wavefront, structure of arrays so that the lanes of a
+// wavefront reading the same slot hit 64 consecutive doubles (bank-conflict free; a per-lane
+// struct with its 40-double stride maps 32 lanes onto 4 banks):
+//   a_j[c] of lane l at [(3 j + c) * 64 + l],  b_j at [(3 DAT_NENV + j) * 64 + l].
+constexpr int ENV_LDS_DOUBLES = 4 * DAT_NENV * 64;
+struct EnvLds {
+  const double* base;
+  int lane;
+  __device__ double a(int j, int c) const {
+    int l = lane;
+    __asm__ volatile("" : "+v"(l));
+    return base[(3 * j + c) * 64 + l];
+  }
+  __device__ double b(int j) const {
+    int l = lane;
+    __asm__ volatile("" : "+v"(l));
+    return base[(3 * DAT_NENV + j) * 64 + l];
+  }
+};
+DAT_HD void env_to_lds(double* base, int lane, const EnvRows& E) {
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) base[(3 * j + c) * 64 + lane] = E.a[j][c];
+    base[(3 * DAT_NENV + j) * 64 + lane] = E.b[j];
+  }
+}
+
+// U-map accessors: get(k) -> Rt_k (9 doubles, row-major) of cone block k
+struct RtPtr {
+  const double* p;  // NB x 9
+  DAT_HD const double* get(int k) const { return p + 9 * k; }
+};
+struct RtLds {
+  const double* base;
+  int off;  // offset of block 0 in doubles
+  __device__ const double* get(int k) const {
+    int j = off;
+    __asm__ volatile("" : "+v"(j));
+    return base + j + 9 * k;
+  }
+};
 
 template <int NB>
 struct QPLane {
   int var;                       // C / cu variant
-  unsigned emask;                // active env slots
+  unsigned emask;                // active env slots (compacted: bits 0 .. k-1)
   int infeasible;
   double kappa, rho, min_fz, max_f, sec;
   double q[NB][3];               // per-block linear term
-  double y0[NB][3];              // interior initial guess (f_eq)
-  double Rt[NB][9];              // U_k = [I; Rt_k],  Rt_k = hat(r_com_k) Rl'
   double atil[6];                // C-ADMM: sum_{j != i} U_j a_j
   double cw[6];                  // DD: linear cost on w = (F_i, M_i)
 };
+
+// row slots an IPM instantiation must cover for a lane whose env mask is emask
+DAT_HD int rows_needed(unsigned emask) { return NBASE + (emask ? 32 - __builtin_clz(emask) : 0); }
+
+// size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6)
+DAT_HD constexpr int best_size(int NB) { return 3 * NB + 18; }
 
 // ------------------------------------------------------------------ shared data
 // k_f, k_m: total force / moment weights; variants: bit 0 build C[0] (kdv = 0), bit 1 build C[1]
@@ -182,26 +239,38 @@ DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st
   }
 }
 
-// env rows (dvl): lhs . dvl >= rhs  <=>  lhs . lin_v(u) + (lhs . bv - rhs) >= 0
+// env rows (dvl): lhs . dvl >= rhs  <=>  lhs . lin_v(u) + (lhs . bv - rhs) >= 0.  Rows the
+// reference would emit are compacted to the front of the slots (P.emask = bits 0 .. k-1); a row
+// with lhs = 0 carries no information and is dropped (infeasible if its constant is negative).
+// Slot writes are predicated on compile-time indices so a register-resident E stays in registers.
 template <int NB>
 DAT_HD void set_env_rows(QPLane<NB>& P, EnvRows& E, const QPShared& S, unsigned mask, const double lhs[DAT_NENV][3],
                          const double rhs[DAT_NENV]) {
-  P.emask = 0u;
   P.infeasible = 0;
 #pragma unroll
   for (int j = 0; j < DAT_NENV; ++j) {
     // inactive slots hold the padding row 0 . x + 1 >= 0
     E.a[j][0] = 0.0; E.a[j][1] = 0.0; E.a[j][2] = 0.0;
     E.b[j] = 1.0;
-    if (!((mask >> j) & 1u)) continue;
-    if (lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0) {
-      if (-rhs[j] < 0.0) P.infeasible = 1;
-      continue;
-    }
-    E.a[j][0] = lhs[j][0]; E.a[j][1] = lhs[j][1]; E.a[j][2] = lhs[j][2];
-    E.b[j] = -rhs[j] + dot3(lhs[j], S.bv);
-    P.emask |= 1u << j;
   }
+  int k = 0;
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) {
+    const bool on = (mask >> j) & 1u;
+    const bool zero = lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0;
+    if (on && zero && -rhs[j] < 0.0) P.infeasible = 1;
+    if (!on || zero) continue;
+    const double bj = -rhs[j] + dot3(lhs[j], S.bv);
+#pragma unroll
+    for (int s = 0; s <= j; ++s) {
+      if (s == k) {
+        E.a[s][0] = lhs[j][0]; E.a[s][1] = lhs[j][1]; E.a[s][2] = lhs[j][2];
+        E.b[s] = bj;
+      }
+    }
+    ++k;
+  }
+  P.emask = (1u << k) - 1u;
 }
 
 // ------------------------------------------------------------------ per-agent data
@@ -221,14 +290,9 @@ DAT_HD void lane_common(QPLane<NB>& P, const double* prm) {
 // Cost: Phi(u) with k = 0.1/n, k_feq ||f_i - f_eq_i||^2, leader terms, <lam, f> + rho/2 ||f||^2
 // - <rho fbar, f>  ==  rho/2 ||f - a||^2 + const with a = fbar - lam / rho.
 // Only f_i carries cones; f_j (j != i) are free and eliminated through (K, atil).
-DAT_HD void lane_cadmm_static(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_i) {
+DAT_HD void lane_cadmm_static(QPLane<1>& P, const double* prm, int i) {
   lane_common(P, prm);
   P.var = (i == 0) ? 1 : 0;
-#pragma unroll
-  for (int c = 0; c < 9; ++c) P.Rt[0][c] = Rt_i[c];
-  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) P.y0[0][c] = feq[c];
 }
 // per-iteration part: penalty rho and a = fbar - lam / rho.  lam, fbar: (3n) agent-major;
 // Rt_all: n x 9.
@@ -267,14 +331,9 @@ DAT_HD void cadmm_free_block(const double* Rt_j, const double* lam_j, const doub
 
 // DD agent i (control/rqp_dd.py:27-505): variables (f_i, F_i, M_i); with w = (F_i, M_i),
 // u = U_i f_i + w.  Cost Phi(u) + k_feq ||f_i - f_eq_i||^2 + c_fi'f_i + (c_Fi, c_Mi)'w.
-DAT_HD void lane_dd_static(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_i) {
+DAT_HD void lane_dd_static(QPLane<1>& P, const double* prm, int i) {
   lane_common(P, prm);
   P.var = (i == 0) ? 1 : 0;
-#pragma unroll
-  for (int c = 0; c < 9; ++c) P.Rt[0][c] = Rt_i[c];
-  const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) P.y0[0][c] = feq[c];
   P.kappa = 2.0 * prm[DAT_P_KFEQ];
 }
 // prices c = (c_fi, c_Fi, c_Mi) (control/rqp_dd.py:718-722)
@@ -288,8 +347,9 @@ DAT_HD void set_dd_price(QPLane<1>& P, const double* prm, int n, int i, const do
 }
 
 // Centralized (control/rqp_centralized.py:27-448): all n agents' forces, k = 0.1, leader terms on.
+// Rt (NB x 9) receives the U-maps of every block.
 template <int NB>
-DAT_HD void lane_cent(QPLane<NB>& P, const double* prm, int n, const double* st) {
+DAT_HD void lane_cent(QPLane<NB>& P, const double* prm, int n, const double* st, double Rt[NB][9]) {
   lane_common(P, prm);
   P.var = 1;
   const double kfeq = prm[DAT_P_KFEQ];
@@ -297,12 +357,9 @@ DAT_HD void lane_cent(QPLane<NB>& P, const double* prm, int n, const double* st)
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const double* feq = prm + DAT_P_FEQ(n) + 3 * k;
-    make_Rt(prm + DAT_P_RCOM(n) + 3 * k, Rl, P.Rt[k]);
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * k, Rl, Rt[k]);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      P.y0[k][c] = feq[c];
-      P.q[k][c] = -2.0 * kfeq * feq[c];
-    }
+    for (int c = 0; c < 3; ++c) P.q[k][c] = -2.0 * kfeq * feq[c];
   }
   P.kappa = 2.0 * kfeq;
 }
@@ -393,23 +450,33 @@ struct IPMOut {
 
 // Solve the reduced QP. MODE_CADMM: NB = 1, implicit free blocks through (K, atil, rho);
 // MODE_DD: NB = 1, w = (F_i, M_i) free with linear cost cw; MODE_CENT: NB = n, no w.
-// y (NB x 3) and w (6) are outputs.  sh / er: accessors of the scenario data and the env rows.
+// NR: row slots processed (NBASE .. DAT_MAXROW); every active env row must sit in a slot < NR.
+// sh / er / rt: accessors of the scenario data, the env rows and the U-maps; y0: interior initial
+// guess (NB x 3, f_eq); best: lane-private record of best_size(NB) doubles.  y (NB x 3) and w (6)
+// are outputs.
 //
-// Register economy (DESIGN.md "Register and LDS budget"): the row loops are branch-free over all
-// NROW slots (an inactive slot is the padding row 0 . x + 1 >= 0 with z = 0, whose complementarity
-// target is zeroed, so it never moves and adds exactly nothing); primal residuals and the scaled
-// cone residual are recomputed where consumed instead of being kept live.
-template <int MODE, int NB, class SH, class ER>
-DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double y[NB][3], double w[6], int max_iter,
-                        double tol) {
+// Register economy (DESIGN.md "Register and LDS budget"): only the iterates (y, w, s, z), the
+// per-iteration factors (NT scalings, D^-1, M, LU) and the current Newton direction live in
+// registers.  The row loops are branch-free over all NR slots (an inactive slot is the padding
+// row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
+// adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
+// terms are recomputed where consumed instead of being kept live.
+template <int MODE, int NB, int NR, class SH, class ER, class RT>
+DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
+                        double y[NB][3], double w[6], double* best, int max_iter, double tol) {
+  static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   IPMOut out;
   out.status = ST_FAILED;
   out.iters = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) { out.pi[r] = 0.0; out.u[r] = 0.0; }
   if (sh.get().infeasible || P.infeasible) {
     out.status = ST_INFEASIBLE;
     return out;
   }
-  const unsigned mask = (unsigned)sh.get().bmask | (P.emask << NBASE);
+  const unsigned emask = P.emask << NBASE;
+  if (emask >> NR) return out;  // an active row outside the instantiated slots: caller error
+  const unsigned mask = (unsigned)sh.get().bmask | emask;
   const int var = P.var;
   const double sec = P.sec, kap = P.kappa;
   const double irho = 1.0 / P.rho;
@@ -418,9 +485,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
   auto Cp = [&]() -> const double* { return sh.get().C[var]; };
   auto cup = [&]() -> const double* { return sh.get().cu[var]; };
   auto ra = [&](int l, int c) -> double {
-    return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.get().a[l >= NBASE ? l - NBASE : 0][c];
+    return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.a(l >= NBASE ? l - NBASE : 0, c);
   };
-  auto rb = [&](int l) -> double { return l < NBASE ? sh.get().bb[l < NBASE ? l : 0] : er.get().b[l >= NBASE ? l - NBASE : 0]; };
+  auto rb = [&](int l) -> double { return l < NBASE ? sh.get().bb[l < NBASE ? l : 0] : er.b(l >= NBASE ? l - NBASE : 0); };
   // row value a_l . (dvl or dwl) of the linear map of u
   auto rowdot = [&](int l, const double* dv, const double* dw) -> double {
     const double* x = l < NWROW ? dw : dv;
@@ -444,7 +511,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
   auto rows_adj = [&](const double* zz, double* o) {  // o = A' zz (u-space)
     double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0};
 #pragma unroll
-    for (int l = 0; l < NROW; ++l) {
+    for (int l = 0; l < NR; ++l) {
       double* g = l < NWROW ? gw : gv;
       g[0] += zz[l] * ra(l, 0); g[1] += zz[l] * ra(l, 1); g[2] += zz[l] * ra(l, 2);
     }
@@ -454,8 +521,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
   auto Kmul = [&](const double* v, double* o) {
     spmv6(sh.get().K, v, o);
     double t[3], t6[6];
-    Ut_apply(P.Rt[0], v, t);
-    U_apply(P.Rt[0], t, t6);
+    Ut_apply(rt.get(0), v, t);
+    U_apply(rt.get(0), t, t6);
 #pragma unroll
     for (int r = 0; r < 6; ++r) o[r] -= t6[r];
   };
@@ -470,7 +537,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
   };
   const double mfz = P.min_fz, mxf = P.max_f;
   // primal residual of cone block k at the current iterate: G y + s - h
-  double sk[NB][9], zk[NB][9], sl[NROW], zl[NROW];
+  double sk[NB][9], zk[NB][9], sl[NR], zl[NR];
   auto rzk_of = [&](int k, double* o) {
     Gy(y[k], o);
 #pragma unroll
@@ -484,7 +551,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       double t[6];
-      U_apply(P.Rt[k], y[k], t);
+      U_apply(rt.get(k), y[k], t);
 #pragma unroll
       for (int r = 0; r < 6; ++r) uo[r] += t[r];
     }
@@ -494,7 +561,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) y[k][c] = P.y0[k][c];
+    for (int c = 0; c < 3; ++c) y[k][c] = y0[3 * k + c];
     double g[9];
     Gy(y[k], g);
 #pragma unroll
@@ -511,7 +578,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
     zk[k][0] = 1.0; zk[k][1] = 1.0; zk[k][5] = 1.0;
   }
 #pragma unroll
-  for (int l = 0; l < NROW; ++l) zl[l] = act(l);
+  for (int l = 0; l < NR; ++l) zl[l] = act(l);
 #pragma unroll
   for (int r = 0; r < 6; ++r) w[r] = 0.0;
   if (MODE == MODE_CADMM) {
@@ -546,13 +613,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
     compute_u(u);
     lin(u, dv, dw);
 #pragma unroll
-    for (int l = 0; l < NROW; ++l) sl[l] = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
+    for (int l = 0; l < NR; ++l) sl[l] = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
   }
 
   // scales for the relative stopping rule
   double nh = 1.0 + fmax(mfz, mxf), nq = 1.0;
 #pragma unroll
-  for (int l = 0; l < NROW; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
+  for (int l = 0; l < NR; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
 #pragma unroll
   for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -560,18 +627,18 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
   for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
 
-  double best_merit = 1e300, best_y[NB][3], best_w[6], best_pi[6], best_u[6];
+  double best_merit = 1e300;
   const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
 
   for (int it = 0;; ++it) {
     // ------------- residuals
-    double u[6], dv[3], dw[3];
-    compute_u(u);
-    lin(u, dv, dw);
+    double dv[3], dw[3];
     double rk[NB][3], Rf[6];
     double dres = 0.0, pres = 0.0, gap = 0.0;
     {
-      double pi[6], az[6];
+      double u[6], pi[6], az[6];
+      compute_u(u);
+      lin(u, dv, dw);
       spmv6(Cp(), u, pi);
       rows_adj(zl, az);
 #pragma unroll
@@ -579,7 +646,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         double ut[3], gz[3];
-        Ut_apply(P.Rt[k], pi, ut);
+        Ut_apply(rt.get(k), pi, ut);
         GTz(zk[k], gz);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -612,7 +679,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
         }
       }
 #pragma unroll
-      for (int l = 0; l < NROW; ++l) {
+      for (int l = 0; l < NR; ++l) {
         pres = fmax(pres, fabs(sl[l] - (rowdot(l, dv, dw) + rb(l))));
         gap += sl[l] * zl[l];
       }
@@ -633,9 +700,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
         for (int k = 0; k < NB; ++k)
 #pragma unroll
-          for (int c = 0; c < 3; ++c) best_y[k][c] = y[k][c];
+          for (int c = 0; c < 3; ++c) best[3 * k + c] = y[k][c];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) { best_w[r] = w[r]; best_pi[r] = pi[r]; best_u[r] = u[r]; }
+        for (int r = 0; r < 6; ++r) {
+          best[3 * NB + r] = w[r];
+          best[3 * NB + 6 + r] = pi[r];
+          best[3 * NB + 12 + r] = u[r];
+        }
       } else if (merit > 1e3 * best_merit || it >= max_iter) {
         break;
       }
@@ -694,10 +765,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       okc = okc && inv3_spd(D, Dinv[k]);
     }
     if (!okc) break;
-    // reciprocal slacks of the rows
-    double isl[NROW];
-#pragma unroll
-    for (int l = 0; l < NROW; ++l) isl[l] = frcp(sl[l]);
     // M (packed) and, for CADMM / CENT, the LU factors of (I + M T); DD: the Cholesky factor of M
     // parked in LU.  (Forming N = (I + M T)^-1 M explicitly would save registers but loses the
     // accuracy the refinement needs once active rows make M huge.)
@@ -708,8 +775,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       {
         double Xv[6] = {0, 0, 0, 0, 0, 0}, Xw[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int l = 0; l < NROW; ++l) {
-          const double wgt = zl[l] * isl[l];
+        for (int l = 0; l < NR; ++l) {
+          const double wgt = zl[l] * frcp(sl[l]);
           double* X = l < NWROW ? Xw : Xv;
           const double a0 = ra(l, 0), a1 = ra(l, 1), a2 = ra(l, 2);
           X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
@@ -746,7 +813,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
         for (int k = 0; k < 21; ++k) LU[k / 6][k % 6] = Lp[k];
       } else {
-        // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho);  N = (I + M T)^-1 M, symmetrised
+        // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho)
         double T[21];
         if (MODE == MODE_CADMM) {
           const double* K = sh.get().K;
@@ -754,12 +821,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
           for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
           // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
           double Dm[6] = {Dinv[0][0] - irho, Dinv[0][1], Dinv[0][2], Dinv[0][3] - irho, Dinv[0][4], Dinv[0][5] - irho};
-          add_UDUt(T, P.Rt[0], Dm, 1.0);
+          add_UDUt(T, rt.get(0), Dm, 1.0);
         } else {
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = 0.0;
 #pragma unroll
-          for (int k = 0; k < NB; ++k) add_UDUt(T, P.Rt[k], Dinv[k], 1.0);
+          for (int k = 0; k < NB; ++k) add_UDUt(T, rt.get(k), Dinv[k], 1.0);
         }
 #pragma unroll
         for (int r = 0; r < 6; ++r)
@@ -774,90 +841,103 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       }
     }
 
-    // core structured solve of (D + U'MU) dx = b (CADMM/CENT) or its DD analogue
-    auto core = [&](const double bk[NB][3], const double* Rfr, const double* bu, double dy[NB][3], double* dwo,
-                    double* du) {
+    // core structured solve of (D + U'MU) dx = b (CADMM/CENT) or its DD analogue.  bu: u-space
+    // part of the right-hand side (has_bu = false: zero); acc: add the solution to the outputs.
+    auto core = [&](const double bk[NB][3], const double* Rfr, const double* bu, bool has_bu, bool acc,
+                    double dyo[NB][3], double* dwo, double* duo) {
+      double dyn[NB][3], dwn[6], dun[6];
       if (MODE == MODE_DD) {
-        double rw[6], Lp[21];
+        double Lp[21];
 #pragma unroll
         for (int k = 0; k < 21; ++k) Lp[k] = LU[k / 6][k % 6];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) rw[r] = -Rfr[r] + bu[r];
-        chol6_solve(Lp, rw);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) du[r] = rw[r];
+        for (int r = 0; r < 6; ++r) dun[r] = -Rfr[r] + (has_bu ? bu[r] : 0.0);
+        chol6_solve(Lp, dun);
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double t[3], v[3];
-          Ut_apply(P.Rt[k], Rfr, t);
+          Ut_apply(rt.get(k), Rfr, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) v[c] = bk[k][c] + t[c];
-          spmv3(Dinv[k], v, dy[k]);
+          spmv3(Dinv[k], v, dyn[k]);
         }
 #pragma unroll
-        for (int r = 0; r < 6; ++r) dwo[r] = du[r];
+        for (int r = 0; r < 6; ++r) dwn[r] = dun[r];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double t[6];
-          U_apply(P.Rt[k], dy[k], t);
+          U_apply(rt.get(k), dyn[k], t);
 #pragma unroll
-          for (int r = 0; r < 6; ++r) dwo[r] -= t[r];
+          for (int r = 0; r < 6; ++r) dwn[r] -= t[r];
         }
-        return;
-      }
-      double bk2[NB][3], yv[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        double t[3], v[3], ut[6];
-        Ut_apply(P.Rt[k], bu, t);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) bk2[k][c] = bk[k][c] + t[c];
-        spmv3(Dinv[k], bk2[k], v);
-        U_apply(P.Rt[k], v, ut);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) yv[r] += ut[r];
-      }
-      double kb[6] = {0, 0, 0, 0, 0, 0};
-      if (MODE == MODE_CADMM) {
-        Kmul(bu, kb);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) yv[r] += (-Rfr[r] + kb[r]) * irho;
-      }
-      double tau[6];
-      spmv6(Mm, yv, tau);
-      lu6_solve(LU, piv, tau);
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        double t[3], v[3];
-        Ut_apply(P.Rt[k], tau, t);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) v[c] = bk2[k][c] - t[c];
-        spmv3(Dinv[k], v, dy[k]);
-      }
-      if (MODE == MODE_CADMM) {
-        double kt[6];
-        Kmul(tau, kt);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) dwo[r] = (-Rfr[r] + kb[r] - kt[r]) * irho;
       } else {
+        double bk2[NB][3], yv[6] = {0, 0, 0, 0, 0, 0}, g6[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-        for (int r = 0; r < 6; ++r) dwo[r] = 0.0;
+        for (int k = 0; k < NB; ++k) {
+          double t[3] = {0, 0, 0}, v[3], ut[6];
+          if (has_bu) Ut_apply(rt.get(k), bu, t);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) bk2[k][c] = bk[k][c] + t[c];
+          spmv3(Dinv[k], bk2[k], v);
+          U_apply(rt.get(k), v, ut);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) yv[r] += ut[r];
+        }
+        if (MODE == MODE_CADMM) {
+          if (has_bu) Kmul(bu, g6);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            g6[r] -= Rfr[r];  // g6 = -Rf + K_{-i} bu
+            yv[r] += g6[r] * irho;
+          }
+        }
+        double tau[6];
+        spmv6(Mm, yv, tau);
+        lu6_solve(LU, piv, tau);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double t[3], v[3];
+          Ut_apply(rt.get(k), tau, t);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) v[c] = bk2[k][c] - t[c];
+          spmv3(Dinv[k], v, dyn[k]);
+        }
+        if (MODE == MODE_CADMM) {
+          double kt[6];
+          Kmul(tau, kt);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dwn[r] = (g6[r] - kt[r]) * irho;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dwn[r] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) dun[r] = (MODE == MODE_CADMM) ? dwn[r] : 0.0;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+          double t[6];
+          U_apply(rt.get(k), dyn[k], t);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dun[r] += t[r];
+        }
       }
 #pragma unroll
-      for (int r = 0; r < 6; ++r) du[r] = (MODE == MODE_CADMM) ? dwo[r] : 0.0;
+      for (int k = 0; k < NB; ++k)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        double t[6];
-        U_apply(P.Rt[k], dy[k], t);
+        for (int c = 0; c < 3; ++c) dyo[k][c] = (acc ? dyo[k][c] : 0.0) + dyn[k][c];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) du[r] += t[r];
+      for (int r = 0; r < 6; ++r) {
+        dwo[r] = (acc ? dwo[r] : 0.0) + dwn[r];
+        duo[r] = (acc ? duo[r] : 0.0) + dun[r];
       }
     };
 
     // Newton direction for complementarity targets rsk (cones, scaled) and, for the rows,
-    // rc_l = s_l z_l + cadd_l (cadd = 0 for the predictor).  Outputs: dy, dw, du, scaled dz of the
-    // cones (dzs_k) and lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k); row dz is zw - (z/s) a.lin(du).
-    double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9], zw[NROW];
+    // rc_l = s_l z_l + cadd_l (cadd = 0 for the predictor; the corrector's second-order term is
+    // formed in place from the predictor's row direction ddva/ddwa and its zw).  Outputs: dy, dw,
+    // du, scaled dz of the cones (dzs_k), lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k) and zw
+    // (row dz is zw - (z/s) a.lin(du)).
+    double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9], zw[NR];
     // tks_k = W^-1 rz_k - lam \ rsk
     auto tks_of = [&](int k, double* t) {
       double rz[9];
@@ -866,7 +946,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
       for (int j = 0; j < 9; ++j) t[j] -= lrs_k[k][j];
     };
-    auto newton = [&](const double rsk[NB][9], const double* cadd) {
+    auto newton = [&](const double rsk[NB][9], bool corr, const double* ddva, const double* ddwa, double sigmu) {
       double bk[NB][3], bu[6];
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -880,13 +960,20 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
         for (int c = 0; c < 3; ++c) bk[k][c] = -rk[k][c] - g3[c];
       }
 #pragma unroll
-      for (int l = 0; l < NROW; ++l) {
+      for (int l = 0; l < NR; ++l) {
+        const double is = frcp(sl[l]);
         const double rzl = sl[l] - (rowdot(l, dv, dw) + rb(l));
-        zw[l] = (zl[l] * rzl - (sl[l] * zl[l] + cadd[l])) * isl[l];
+        double cadd = 0.0;
+        if (corr) {
+          const double a = rowdot(l, ddva, ddwa);
+          cadd = act(l) * ((-rzl + a) * (zw[l] - zl[l] * is * a) - sigmu);
+        }
+        zw[l] = (zl[l] * rzl - (sl[l] * zl[l] + cadd)) * is;
       }
       rows_adj(zw, bu);
-      core(bk, Rf, bu, dy, dwv, du);
-      for (int ref = 0; ref < 2; ++ref) {
+      core(bk, Rf, bu, true, false, dy, dwv, du);
+#pragma unroll 1
+      for (int ref = 0; ref < NREF; ++ref) {
         // linearised dual residual of the full system at (dy, dw); refine
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -896,19 +983,26 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
           for (int j = 0; j < 9; ++j) dzs_k[k][j] = tks[j] + g9[j];
         }
-        double ddv[3], ddw[3], dzl[NROW], dpi[6], adz[6];
+        double ddv[3], ddw[3], dpi[6];
         lin(du, ddv, ddw);
-#pragma unroll
-        for (int l = 0; l < NROW; ++l) dzl[l] = zw[l] - zl[l] * isl[l] * rowdot(l, ddv, ddw);
         spmv6(Cp(), du, dpi);
-        rows_adj(dzl, adz);
+        {
+          double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0}, adz[6];
 #pragma unroll
-        for (int r = 0; r < 6; ++r) dpi[r] -= adz[r];
+          for (int l = 0; l < NR; ++l) {
+            const double dzl = zw[l] - zl[l] * frcp(sl[l]) * rowdot(l, ddv, ddw);
+            double* g = l < NWROW ? gw : gv;
+            g[0] += dzl * ra(l, 0); g[1] += dzl * ra(l, 1); g[2] += dzl * ra(l, 2);
+          }
+          adj(gv, gw, adz);
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dpi[r] -= adz[r];
+        }
         double ek[NB][3], ef[6];
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double ut[3], g3[3];
-          Ut_apply(P.Rt[k], dpi, ut);
+          Ut_apply(rt.get(k), dpi, ut);
           gs_tmul(k, dzs_k[k], g3);
 #pragma unroll
           for (int c = 0; c < 3; ++c) ek[k][c] = -(kap * dy[k][c] + ut[c] + g3[c] + rk[k][c]);
@@ -925,14 +1019,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
           for (int r = 0; r < 6; ++r) ef[r] = 0.0;
         }
-        double zero6[6] = {0, 0, 0, 0, 0, 0}, cy[NB][3], cw6[6], cu6[6];
-        core(ek, ef, zero6, cy, cw6, cu6);
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-#pragma unroll
-          for (int c = 0; c < 3; ++c) dy[k][c] += cy[k][c];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) { dwv[r] += cw6[r]; du[r] += cu6[r]; }
+        core(ek, ef, nullptr, false, true, dy, dwv, du);
       }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -947,7 +1034,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
     auto row_dirs = [&](int l, const double* ddv, const double* ddw, double& ds, double& dz) {
       const double a = rowdot(l, ddv, ddw);
       ds = -(sl[l] - (rowdot(l, dv, dw) + rb(l))) + a;
-      dz = zw[l] - zl[l] * isl[l] * a;
+      dz = zw[l] - zl[l] * frcp(sl[l]) * a;
     };
     auto step_len = [&]() {
       double a = 1e300;
@@ -966,7 +1053,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       double ddv[3], ddw[3];
       lin(du, ddv, ddw);
 #pragma unroll
-      for (int l = 0; l < NROW; ++l) {
+      for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
         if (ds < 0) a = fmin(a, -sl[l] * frcp(ds));
@@ -986,7 +1073,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       double ddv[3], ddw[3];
       lin(du, ddv, ddw);
 #pragma unroll
-      for (int l = 0; l < NROW; ++l) {
+      for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
         g += (sl[l] + al * ds) * (zl[l] + al * dz);
@@ -996,16 +1083,14 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 
     // predictor
     {
-      double rsk[NB][9], cadd[NROW];
+      double rsk[NB][9];
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         rsk[k][0] = lamk[k][0] * lamk[k][0];
         soc_jprod(lamk[k] + 1, lamk[k] + 1, rsk[k] + 1);
         soc_jprod(lamk[k] + 5, lamk[k] + 5, rsk[k] + 5);
       }
-#pragma unroll
-      for (int l = 0; l < NROW; ++l) cadd[l] = 0.0;
-      newton(rsk, cadd);
+      newton(rsk, false, nullptr, nullptr, 0.0);
     }
     {
       const double aaff = fmin(1.0, step_len());
@@ -1014,7 +1099,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       sig = fmax(0.0, fmin(1.0, sig * sig * sig));
       const double sigmu = sig * gap * ideg;
       // corrector: rs = lam o lam + dss_aff o dzs_aff - sig mu e
-      double rsk[NB][9], cadd[NROW];
+      double rsk[NB][9];
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         double dss[9], c1[4], c2[4];
@@ -1030,17 +1115,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
         rsk[k][1] -= sigmu;
         rsk[k][5] -= sigmu;
       }
-      {
-        double ddv[3], ddw[3];
-        lin(du, ddv, ddw);
-#pragma unroll
-        for (int l = 0; l < NROW; ++l) {
-          double ds, dz;
-          row_dirs(l, ddv, ddw, ds, dz);
-          cadd[l] = act(l) * (ds * dz - sigmu);
-        }
-      }
-      newton(rsk, cadd);
+      double ddva[3], ddwa[3];
+      lin(du, ddva, ddwa);
+      newton(rsk, true, ddva, ddwa, sigmu);
     }
     double alpha = fmin(1.0, 0.99 * step_len());
     // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
@@ -1071,7 +1148,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
       double ddv[3], ddw[3];
       lin(du, ddv, ddw);
 #pragma unroll
-      for (int l = 0; l < NROW; ++l) {
+      for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
         sl[l] += alpha * ds;
@@ -1085,13 +1162,25 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const QPLane<NB>& P, double 
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[k][c] = best_y[k][c];
+      for (int c = 0; c < 3; ++c) y[k][c] = best[3 * k + c];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) { w[r] = best_w[r]; out.pi[r] = best_pi[r]; out.u[r] = best_u[r]; }
+    for (int r = 0; r < 6; ++r) {
+      w[r] = best[3 * NB + r];
+      out.pi[r] = best[3 * NB + 6 + r];
+      out.u[r] = best[3 * NB + 12 + r];
+    }
     out.status = best_merit < 1e2 * tol ? ST_OPTIMAL : ST_INACCURATE;
   }
   return out;
 }
 
+// Solve with the smallest row-slot instantiation that covers every lane of the wavefront
+// (nr_wave: wave-uniform maximum of rows_needed over the lanes taking part).
+template <int MODE, int NB, class SH, class ER, class RT>
+DAT_HD IPMOut ipm_solve_rows(int nr_wave, const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
+                             const double* y0, double y[NB][3], double w[6], double* best, int max_iter, double tol) {
+  if (nr_wave <= NBASE) return ipm_solve<MODE, NB, NBASE>(sh, er, rt, P, y0, y, w, best, max_iter, tol);
+  return ipm_solve<MODE, NB, DAT_MAXROW>(sh, er, rt, P, y0, y, w, best, max_iter, tol);
+}
 
 }  // namespace dat

@@ -33,14 +33,16 @@ int cent_nb(const double* prm, const double* st, const double* acc, const double
   QPShared S;
   build_shared(S, prm, NB, st, acc, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
   QPLane<NB> P;
-  lane_cent(P, prm, NB, st);
+  double Rt[NB][9];
+  lane_cent(P, prm, NB, st, Rt);
   double lhs[DAT_NENV][3], rhs[DAT_NENV];
   unsigned mask;
   env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
   EnvRows E;
   set_env_rows(P, E, S, mask, lhs, rhs);
-  double y[NB][3], w[6];
-  IPMOut o = ipm_solve<MODE_CENT, NB>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
+  double y[NB][3], w[6], best[best_size(NB)];
+  IPMOut o = ipm_solve_rows<MODE_CENT, NB>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+                                           RtPtr{&Rt[0][0]}, P, prm + DAT_P_FEQ(NB), y, w, best, 50, HS_TOL);
   for (int k = 0; k < NB; ++k)
     for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
   *iters = o.iters;
@@ -61,15 +63,17 @@ int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, c
   QPShared S;
   build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
   QPLane<1> P;
-  lane_cadmm_static(P, prm, n, i, Rt_all + 9 * i);
+  lane_cadmm_static(P, prm, i);
   double lhs[DAT_NENV][3], rhs[DAT_NENV];
   unsigned mask;
   env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
   EnvRows E;
   set_env_rows(P, E, S, mask, lhs, rhs);
   lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
-  double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_CADMM, 1>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
+  double y[1][3], w[6], best[best_size(1)];
+  IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+                                           RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50,
+                                           HS_TOL);
   for (int j = 0; j < n; ++j) {
     if (j == i) {
       for (int c = 0; c < 3; ++c) f_out[3 * j + c] = y[0][c];
@@ -89,15 +93,16 @@ int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, cons
   QPShared S;
   build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
   QPLane<1> P;
-  lane_dd_static(P, prm, n, i, Rt);
+  lane_dd_static(P, prm, i);
   set_dd_price(P, prm, n, i, c9);
   double lhs[DAT_NENV][3], rhs[DAT_NENV];
   unsigned mask;
   env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
   EnvRows E;
   set_env_rows(P, E, S, mask, lhs, rhs);
-  double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_DD, 1>(PlainRef<QPShared>{&S}, PlainRef<EnvRows>{&E}, P, y, w, 50, HS_TOL);
+  double y[1][3], w[6], best[best_size(1)];
+  IPMOut o = ipm_solve_rows<MODE_DD, 1>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+                                        RtPtr{Rt}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50, HS_TOL);
   for (int c = 0; c < 3; ++c) x_out[c] = y[0][c];
   for (int c = 0; c < 6; ++c) x_out[3 + c] = w[c];
   *iters = o.iters;
