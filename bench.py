@@ -28,9 +28,26 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (AMD spec)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md
-# FP64 flops per IPM iteration of the reduced agent QP, executed count of the structured kernel
-# (DESIGN.md "Roofline accounting"): fixed part + per u-row part.
-FLOPS_PER_IPM_ITER = 7600.0
+# Algorithmic FP64 flops per IPM iteration of the reduced C-ADMM agent QP:
+# F_it(R) = FLOPS_FIXED + FLOPS_PER_ROW * R, R = active constraint rows of the solve.  The kernel
+# counts IPM iterations and IPM iterations x active rows on device (dat_get_counters).
+FLOPS_FIXED = 7267.0
+FLOPS_PER_ROW = 283.0
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def traffic_per_launch(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/summarize_prof.py),
+    if it was taken on this workload; None otherwise."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    e = t.get(kernel)
+    if not e or e.get("workload") != workload:
+        return None, None
+    return e["bytes_per_launch"], e.get("source")
 
 
 def parse():
@@ -75,6 +92,28 @@ def cpu_baseline(n: int, budget_s: float):
                       f"states, {solves} agent QPs in {dt:.1f} s"}
 
 
+def shard(rank: int, batch: int, num_forests: int):
+    """Scenario range of one rank (weak scaling): global scenario ids [rank B, (rank + 1) B); scenario
+    s drives forest s mod num_forests; start states from a per-rank seed."""
+    ids = np.arange(batch) + rank * batch
+    return ids % num_forests, 1000 + rank
+
+
+def combine_ranks(dist, world: int, tot: np.ndarray, metrics: np.ndarray, device):
+    """Sum of the work counters, max of the elapsed time, all-gather of the per-scenario metrics.
+    The only collectives of the run (RCCL over xGMI with the nccl backend; gloo on CPU in tests)."""
+    import torch
+
+    t = torch.tensor(tot, dtype=torch.float64, device=device)
+    mx = t.clone()
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    gm = torch.tensor(metrics, dtype=torch.float64, device=device)
+    gath = [torch.empty_like(gm) for _ in range(world)]
+    dist.all_gather(gath, gm)
+    return t.cpu().numpy(), mx.cpu().numpy(), torch.cat(gath).cpu().numpy()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,11 +129,12 @@ def main():
     from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
 
     n, B = args.n, args.batch
-    rng = np.random.default_rng(1000 + rank)
+    scen_forest, seed = shard(rank, B, args.forests)
+    rng = np.random.default_rng(seed)
     forests = [Forest.seeded(s) for s in range(args.forests)]
     states = scenarios.forest_start_states(n, B, rng)
     eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
-    eng.set_forests(forests, (np.arange(B) + rank * B) % len(forests))
+    eng.set_forests(forests, scen_forest)
     eng.set_state(states, np.zeros(B, dtype=np.int32))
     eng.closed_loop(args.warmup)
     eng.reset_counters()
@@ -114,28 +154,21 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    qps, ipm, hl_steps, hl_ms = eng.counters()
+    work = eng.work()
+    qps, ipm, hl_steps, hl_ms = work["qp_solves"], work["ipm_iters"], work["hl_steps"], work["hl_kernel_ms"]
+    row_it = work["ipm_row_iters"]
     # per-scenario metrics of the last step (all-gathered over ranks: the only collective)
     res = eng.control(None, None)
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
-    tot = np.array([qps, ipm, hl_ms, elapsed], dtype=np.float64)
+    tot = np.array([qps, ipm, hl_ms, elapsed, row_it], dtype=np.float64)
     if dist is not None:
-        import torch
-
-        t = torch.tensor(tot, device=f"cuda:{local}")
-        mx = t.clone()
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        gm = torch.tensor(local_metrics, device=f"cuda:{local}")
-        gath = [torch.empty_like(gm) for _ in range(world)]
-        dist.all_gather(gath, gm)
-        all_metrics = torch.cat(gath).cpu().numpy()
-        qps_all, ipm_all = float(t[0]), float(t[1])
-        elapsed = float(mx[3])
+        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, f"cuda:{local}")
+        qps_all, ipm_all, row_all = float(sums[0]), float(sums[1]), float(sums[4])
+        elapsed = float(maxs[3])
         hl_ms_rank0 = float(tot[2])
     else:
         all_metrics = local_metrics
-        qps_all, ipm_all, hl_ms_rank0 = float(qps), float(ipm), float(hl_ms)
+        qps_all, ipm_all, row_all, hl_ms_rank0 = float(qps), float(ipm), float(row_it), float(hl_ms)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -143,8 +176,11 @@ def main():
     value = qps_all / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     launch_ms = hl_ms_rank0 / max(hl_steps, 1)
-    flops_launch = (ipm / max(hl_steps, 1)) * FLOPS_PER_IPM_ITER
+    # rank 0's own launches: flops of one launch / its average duration (HIP events)
+    flops_launch = (FLOPS_FIXED * ipm + FLOPS_PER_ROW * row_it) / max(hl_steps, 1)
     achieved_tflops = flops_launch / (launch_ms * 1e-3) / 1e12
+    workload = f"C4: {args.mode} n={n}, forest env, {B} closed-loop scenarios per GPU"
+    traffic, traffic_src = traffic_per_launch("k_cadmm", workload)
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
         "value": value,
@@ -158,14 +194,17 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded forests 0..63, randomized C4 start states)",
-        "config": {"workload": f"C4: {args.mode} n={n}, forest env, {B} closed-loop scenarios per GPU",
+        "config": {"workload": workload,
                    "n": n, "scenarios_per_gpu": B, "hl_every": 10, "dt": 1e-3, "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
+                  "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
                   "hl_kernel_ms_per_step": launch_ms},
-        "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": None,
-                     "kernel": "k_cadmm", "flops_per_ipm_iter": FLOPS_PER_IPM_ITER},
+        "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src, "kernel": "k_cadmm", "launch_ms": launch_ms,
+                     "flops_per_launch": flops_launch,
+                     "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"},
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s)

@@ -180,10 +180,18 @@ class BatchedController:
         return lhs, rhs, nr, col.astype(bool), md
 
     def counters(self):
-        q, it, hs, ms = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_double()
-        L.check(self._lib.dat_get_counters(self._h, ctypes.byref(q), ctypes.byref(it), ctypes.byref(hs),
-                                           ctypes.byref(ms)))
-        return q.value, it.value, hs.value, ms.value
+        """(agent-QP solves, IPM iterations, HL steps, summed HL kernel ms) since the last reset."""
+        w = self.work()
+        return w["qp_solves"], w["ipm_iters"], w["hl_steps"], w["hl_kernel_ms"]
+
+    def work(self) -> dict:
+        """Device work counters since the last reset (dat_get_counters)."""
+        q, it, rw, hs, ms = (ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(),
+                             ctypes.c_double())
+        L.check(self._lib.dat_get_counters(self._h, ctypes.byref(q), ctypes.byref(it), ctypes.byref(rw),
+                                           ctypes.byref(hs), ctypes.byref(ms)))
+        return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
+                "hl_kernel_ms": ms.value}
 
     def reset_counters(self) -> None:
         L.check(self._lib.dat_reset_counters(self._h))

@@ -71,7 +71,7 @@ struct KArgs {
   double* mind;
   unsigned char* col;
   double* err;
-  unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations
+  unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   const double* prm = nullptr;
   double* lam = nullptr;
   int iter = 0, qstat = ST_OPTIMAL;
-  long long my_ipm = 0, my_qp = 0;
+  long long my_ipm = 0, my_qp = 0, my_rowit = 0;
   EnvOut env;
   env.collision = 0;
   env.min_env_dist = 0.0;
@@ -195,6 +195,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
       double y[1][3], w[6];
       IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
+      my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
       if (o.status == ST_OPTIMAL) {
@@ -314,14 +315,16 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     a.mind[sc] = md;
   }
   // work counters: one atomic per lane group
-  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm;
+  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
+    rw += __shfl_xor(rw, off);
   }
   if (lane == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
+    atomicAdd(a.counters + 2, rw);
   }
 }
 
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   const double* prm = nullptr;
   double prev[9];
   int iter = 0, qstat = ST_OPTIMAL;
-  long long my_ipm = 0, my_qp = 0;
+  long long my_ipm = 0, my_qp = 0, my_rowit = 0;
   EnvOut env;
   env.collision = 0;
   env.min_env_dist = 0.0;
@@ -552,6 +555,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       double y[1][3], w[6];
       IPMOut o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
+      my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
       if (o.status == ST_OPTIMAL) {
@@ -647,14 +651,16 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     a.col[sc] = (unsigned char)coll;
     a.mind[sc] = md;
   }
-  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm;
+  unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
+    rw += __shfl_xor(rw, off);
   }
   if (lane == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
+    atomicAdd(a.counters + 2, rw);
   }
 }
 
@@ -666,7 +672,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = sc < a.B;
   const int n = NB;
-  unsigned long long q = 0, ip = 0;
+  unsigned long long q = 0, ip = 0, rw = 0;
   const double* prm = valid ? prm_of(a, sc) : a.params;
   QPShared S;
   QPLane<NB> P;
@@ -697,6 +703,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
                                              IPM_MAX_ITER, IPM_TOL);
     q = 1;
     ip = o.iters;
+    rw = (unsigned long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
     double* pf = a.pf + (size_t)sc * 3 * n;
     if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
       for (int k = 0; k < NB; ++k)
@@ -710,10 +717,12 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
+    rw += __shfl_xor(rw, off);
   }
   if (threadIdx.x == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
+    atomicAdd(a.counters + 2, rw);
   }
 }
 
@@ -1019,7 +1028,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   rc |= dalloc(h, &h->qstatus, B * n);
   rc |= dalloc(h, &h->mind, B);
   rc |= dalloc(h, &h->col, B);
-  rc |= dalloc(h, &h->counters, 2);
+  rc |= dalloc(h, &h->counters, 3);
   if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
   if (c.mode == DAT_MODE_CADMM) {
     rc |= dalloc(h, &h->cf, B * n * N3);
@@ -1226,14 +1235,16 @@ int dat_closed_loop(dat_handle* h, int hl_steps) {
   return 0;
 }
 
-int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* hl_steps, double* hl_kernel_ms) {
+int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* ipm_row_iters,
+                     long long* hl_steps, double* hl_kernel_ms) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  unsigned long long c[2] = {0, 0};
+  unsigned long long c[3] = {0, 0, 0};
   HIPCHK(hipMemcpyAsync(c, h->counters, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (qp_solves) *qp_solves = (long long)c[0];
   if (ipm_iters) *ipm_iters = (long long)c[1];
+  if (ipm_row_iters) *ipm_row_iters = (long long)c[2];
   if (hl_steps) *hl_steps = h->hl_steps;
   if (hl_kernel_ms) *hl_kernel_ms = h->hl_ms;
   return 0;
@@ -1242,7 +1253,7 @@ int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, 
 int dat_reset_counters(dat_handle* h) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  HIPCHK(hipMemsetAsync(h->counters, 0, 2 * sizeof(unsigned long long), h->stream));
+  HIPCHK(hipMemsetAsync(h->counters, 0, 3 * sizeof(unsigned long long), h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
   h->hl_ms = 0.0;

@@ -249,6 +249,47 @@ DAT_HD bool chol6(const double* A, double* L) {
   }
   return true;
 }
+// Same factorization with the true diagonal kept (L[sp6(j,j)] = L_jj): the factor is used as a
+// multiplier (L v, L' v), not for substitution.
+DAT_HD bool chol6_lower(const double* A, double* L) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double s = A[sp6(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= L[sp6(j, k)] * L[sp6(j, k)];
+    if (!(s > 0)) return false;
+    const double d = sqrt(s);
+    const double id = frcp(d);
+    L[sp6(j, j)] = d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double t = A[sp6(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= L[sp6(i, k)] * L[sp6(j, k)];
+      L[sp6(i, j)] = t * id;
+    }
+  }
+  return true;
+}
+// o = L v / o = L' v for a packed lower factor with true diagonal (o may not alias v)
+DAT_HD void trmv6(const double* L, const double* v, double* o) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k <= r; ++k) s += L[sp6(r, k)] * v[k];
+    o[r] = s;
+  }
+}
+DAT_HD void trmtv6(const double* L, const double* v, double* o) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = r; k < 6; ++k) s += L[sp6(k, r)] * v[k];
+    o[r] = s;
+  }
+}
 DAT_HD void chol6_solve(const double* L, double* b) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {

@@ -49,6 +49,11 @@ typedef struct dat_config {
 } dat_config;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */
+/* dat_create replaces the controller constructors (RQPCADMMController.__init__
+ * control/rqp_cadmm.py:513-538, RQPDDController.__init__ control/rqp_dd.py:561-586,
+ * RQPCentralizedController.__init__ control/rqp_centralized.py:46-132): it allocates the
+ * persistent warm state the reference keeps in Python objects (f, f_mean, lambda
+ * control/rqp_cadmm.py:569-580; lambda_F, lambda_M control/rqp_dd.py:618-632; prev_f). */
 void dat_default_config(dat_config* cfg);
 int dat_create(const dat_config* cfg, dat_handle** out);
 int dat_destroy(dat_handle* h);
@@ -56,23 +61,36 @@ const char* dat_last_error(void); /* thread-local message of the last failing ca
 int dat_device_count(void);
 
 /* ---- problem data ------------------------------------------------------------------------ */
-/* params: per_scenario ? B x DAT_PARAM_SIZE(n) : DAT_PARAM_SIZE(n) (broadcast) */
+/* params: per_scenario ? B x DAT_PARAM_SIZE(n) : DAT_PARAM_SIZE(n) (broadcast).  The block holds
+ * RQPParameters' derived fields (system/rigid_quadrotor_payload.py:48-84), f_eq
+ * (_set_system_constants, control/rqp_cadmm.py:142-190) and the controller constants
+ * (_set_controller_constants, control/rqp_cadmm.py:192-236, rqp_centralized.py:182-225).
+ * Resets the warm state to the constructor's (f = f_eq, lambda = 0). */
 int dat_set_params(dat_handle* h, const double* params, int per_scenario);
 /* forests: num_forests layouts; tree_offsets[num_forests+1] index rows of tree_pos (T x 3);
  * scenario_forest[B] selects a layout per scenario (NULL: all use layout 0, -1: no env);
  * mountain[num_forests x DAT_MOUNTAIN_SIZE] for the desired-acceleration law.  num_forests = 0
  * removes the environment (env = None in the reference). */
+/* Replaces the env object handed to the controllers (Forest, example/env_forest.py:35-85) and the
+ * hppfcl queries made through it (centralized_distance / distributed_distance :139-212). */
 int dat_set_forests(dat_handle* h, int num_forests, const int* tree_offsets, const double* tree_pos,
                     const int* scenario_forest, const double* mountain);
-int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res); /* set_force_err_tolerance */
-int dat_set_max_iter(dat_handle* h, int max_iter);                       /* set_max_iter           */
-int dat_reset_warm_start(dat_handle* h); /* controller construction state (f = f_eq, lambda = 0) */
+/* set_force_err_tolerance: control/rqp_cadmm.py:683-685, control/rqp_dd.py:760-761 */
+int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res);
+/* set_max_iter: control/rqp_cadmm.py:687-688, control/rqp_dd.py:763-764 */
+int dat_set_max_iter(dat_handle* h, int max_iter);
+/* _set_warm_start: control/rqp_cadmm.py:577-580, control/rqp_dd.py:628-632 */
+int dat_reset_warm_start(dat_handle* h);
 
 /* ---- state ------------------------------------------------------------------------------ */
 int dat_set_state(dat_handle* h, const double* state /* B x DAT_STATE_SIZE(n) */, const int* counters /* B or NULL */);
 int dat_get_state(dat_handle* h, double* state, int* counters);
 
 /* ---- one high-level control step for every scenario ---------------------------------------
+ * Replaces controller.control(state, acc_des) -> (f_des, SolverStatistics):
+ *   RQPCADMMController.control   control/rqp_cadmm.py:631-675  (agent solves :482-501)
+ *   RQPDDController.control      control/rqp_dd.py:695-752     (agent solves :475-505)
+ *   RQPCentralizedController.control control/rqp_centralized.py:436-448
  * state: B x DAT_STATE_SIZE(n) or NULL (use the device-resident state);
  * acc_des: B x 6 (dvl_des, dwl_des) or NULL (forest law example/rqp_example.py:33-59 on device).
  * Outputs (any may be NULL): f_des B x 3n (agent-major, the forces the controller returns),
@@ -82,20 +100,27 @@ int dat_control_step(dat_handle* h, const double* state, const double* acc_des, 
                      int* qp_status, double* min_env_dist, unsigned char* collision, double* err_seq);
 
 /* ---- rollout: `steps` simulation steps (SO(3) PD low level + rigid-body dynamics) ---------
+ * Replaces RQPLowLevelController.control (control/rqp_centralized.py:518-535) followed by
+ * RQPDynamics.integrate (system/rigid_quadrotor_payload.py:271-276) per simulation step.
  * f_des: B x 3n held constant over the steps, or NULL to use the last control step's output. */
 int dat_rollout(dat_handle* h, int steps, const double* f_des);
 
-/* ---- device-resident closed loop: hl_steps x (desired acceleration + control step +
+/* ---- device-resident closed loop (the loop of example/rqp_example.py:120-131 with the desired
+ * acceleration of :33-59): hl_steps x (desired acceleration + control step +
  * hl_every rollout steps); inputs already in HBM, nothing copied per step. */
 int dat_closed_loop(dat_handle* h, int hl_steps);
 
-/* ---- counters since the last reset: agent-QP solves, IPM iterations, control steps,
- * and the summed device time of the high-level kernels [ms] (HIP events on the handle stream). */
-int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* hl_steps, double* hl_kernel_ms);
+/* ---- counters since the last reset: agent-QP solves, IPM iterations, IPM iterations x active
+ * constraint rows (for the flop model of DESIGN.md 3.1), control steps, and the summed device time
+ * of the high-level kernels [ms] (HIP events on the handle stream).  Any pointer may be NULL. */
+int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* ipm_row_iters,
+                     long long* hl_steps, double* hl_kernel_ms);
 int dat_reset_counters(dat_handle* h);
 int dat_synchronize(dat_handle* h);
 
 /* ---- raw batched kernels (tests / benchmarking of single pieces) ---------------------------
+ * dat_env_rows: _set_collision_avoidance_cbf_parameters (control/rqp_cadmm.py:307-373,
+ * control/rqp_centralized.py:280-337) for every (scenario, agent).
  * Env CBF rows for every (scenario, agent) of the current state: lhs B x n x 10 x 3, rhs
  * B x n x 10, nrow B x n, collision B x n, min_dist B x n (agent = -1 row when centralized). */
 int dat_env_rows(dat_handle* h, double* lhs, double* rhs, int* nrow, unsigned char* collision, double* min_dist);
