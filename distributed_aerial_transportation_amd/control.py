@@ -193,6 +193,14 @@ class BatchedController:
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
                 "hl_kernel_ms": ms.value}
 
+    def class_work(self, env_class: int) -> dict:
+        """C-ADMM only: work counters and summed kernel time of one env class (0: scenarios whose agent
+        QPs carry no env CBF row in the step, 1: the others) -- dat_get_class_counters."""
+        q, it, rw, ms = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_double()
+        L.check(self._lib.dat_get_class_counters(self._h, int(env_class), ctypes.byref(q), ctypes.byref(it),
+                                                 ctypes.byref(rw), ctypes.byref(ms)))
+        return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "kernel_ms": ms.value}
+
     def reset_counters(self) -> None:
         L.check(self._lib.dat_reset_counters(self._h))
 

@@ -72,6 +72,10 @@ struct KArgs {
   unsigned char* col;
   double* err;
   unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
+                                 // (C-ADMM: [3k + .] per env class k of k_cadmm<ENV = k>)
+  int* need;                     // C-ADMM: per-scenario env class of the step (k_env_class)
+  int* slist;                    // C-ADMM: scenario ids, class 0 first, then class 1 (k_bucket)
+  int* scount;                   // C-ADMM: class sizes [2]
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)
@@ -95,12 +99,23 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 // ------------------------------------------------------------------------------------------------
 // C-ADMM
 // ------------------------------------------------------------------------------------------------
+// A control step runs as four launches:
+//   k_env_class   one lane per agent: env CBF rows of the step (they depend on the state only, so
+//                 they are fixed for the whole ADMM loop, control/rqp_cadmm.py:305), per-scenario
+//                 env class (1 if any agent's QP carries an env row), collision, min env distance;
+//   k_bucket      stable partition of the scenario ids by class;
+//   k_cadmm<0>    the scenarios without env rows: 3 row slots, no env image in LDS, so the IPM's
+//                 register budget and the workgroup's LDS are sized for the common case;
+//   k_cadmm<1>    the scenarios with env rows (13 row slots, env image in LDS).
+// Each scenario's arithmetic does not depend on the scenarios it shares a wavefront with (padding
+// rows add exact zeros), so the regrouping does not change any result.
+//
 // LDS layout of one 64-lane block (G = floor(64/n) scenarios).  Per-lane records use an odd
 // stride in doubles so that the 32 lanes of a ds_read_b64 group fall on distinct bank pairs.
 //   fx   NT x FXS  agent copies f^(i) (FXS = 3n rounded up to odd)    fbar G x 3n  consensus mean
 //   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x RDS (9)  per-lane exchange slots
 //   sh   G x QPShared (u-maps, packed Hessians, base rows, K)
-//   env  EnvLds image (structure of arrays over the 64 lanes)        done G ints
+//   env  EnvLds image (structure of arrays over the 64 lanes; class-1 kernel only)   done G ints
 constexpr int RDS = 9;
 __host__ __device__ inline int fx_stride(int n) { return (3 * n) | 1; }
 struct CadmmLds {
@@ -109,12 +124,12 @@ struct CadmmLds {
   double* env;
   int* done;
 };
-__host__ __device__ inline size_t cadmm_lds_bytes(int n) {
+__host__ __device__ inline size_t cadmm_lds_bytes(int n, bool env) {
   const int G = 64 / n, NT = G * n;
   return sizeof(double) * ((size_t)NT * fx_stride(n) + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * RDS) +
-         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES + sizeof(int) * 64;
+         sizeof(QPShared) * (size_t)G + (env ? sizeof(double) * ENV_LDS_DOUBLES : 0) + sizeof(int) * 64;
 }
-__device__ inline CadmmLds cadmm_carve(double* smem, int n) {
+__device__ inline CadmmLds cadmm_carve(double* smem, int n, bool env) {
   const int G = 64 / n, NT = G * n;
   CadmmLds L;
   L.fx = smem;
@@ -123,19 +138,106 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n) {
   L.red = L.Rt + G * 9 * n;
   L.sh = (QPShared*)(L.red + 64 * RDS);
   L.env = (double*)(L.sh + G);
-  L.done = (int*)(L.env + ENV_LDS_DOUBLES);
+  L.done = (int*)(L.env + (env ? ENV_LDS_DOUBLES : 0));
   return L;
 }
 
+// the QP must carry env rows: a nonzero row, or an all-zero row with a positive right-hand side
+// (0 >= rhs > 0 makes the reference's QP infeasible; set_env_rows flags it)
+__device__ inline bool env_rows_needed(unsigned emask, const double lhs[DAT_NENV][3], const double rhs[DAT_NENV]) {
+  bool need = false;
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) {
+    const bool on = (emask >> j) & 1u;
+    const bool zero = lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0;
+    need = need || (on && (!zero || rhs[j] > 0.0));
+  }
+  return need;
+}
+
+__global__ __launch_bounds__(64) void k_env_class(KArgs a) {
+  __shared__ int nd[64], cl[64];
+  __shared__ double md[64];
+  const int n = a.n, G = 64 / n, NT = G * n;
+  const int lane = threadIdx.x;
+  const int ls = lane / n, i = lane - ls * n;
+  const int sc = blockIdx.x * G + ls;
+  const bool valid = (lane < NT) && (sc < a.B);
+  int need = 0, col = 0;
+  double dist = 1e300;
+  if (valid) {
+    const double* prm = prm_of(a, sc);
+    const double* trees;
+    int nt;
+    unsigned emask;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    EnvOut e = env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+    need = env_rows_needed(emask, lhs, rhs) ? 1 : 0;
+    col = e.collision;
+    dist = e.min_env_dist;
+  }
+  nd[lane] = need;
+  cl[lane] = col;
+  md[lane] = dist;
+  __syncthreads();
+  if (valid && i == 0) {
+    int any = 0, c = 0;
+    double m = prm_of(a, sc)[DAT_P_VISR];
+    for (int k = 0; k < n; ++k) {
+      any |= nd[ls * n + k];
+      c |= cl[ls * n + k];
+      m = fmin(m, md[ls * n + k]);
+    }
+    a.need[sc] = any;
+    a.col[sc] = (unsigned char)c;
+    a.mind[sc] = m;
+  }
+}
+
+// Stable partition of the scenario ids by need[]: list = [class 0 ..., class 1 ...], count[k] =
+// size of class k.  One 1024-thread workgroup; each thread owns a contiguous chunk.
+__global__ __launch_bounds__(1024) void k_bucket(int B, const int* need, int* list, int* count) {
+  __shared__ int s[1024];
+  const int t = threadIdx.x;
+  const int chunk = (B + 1023) / 1024;
+  const int lo = min(B, t * chunk), hi = min(B, lo + chunk);
+  int c1 = 0;
+  for (int k = lo; k < hi; ++k) c1 += need[k] != 0;
+  s[t] = c1;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = t >= off ? s[t - off] : 0;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  const int tot1 = s[1023], tot0 = B - tot1;
+  int o1 = s[t] - c1;  // class-1 ids before this chunk
+  int o0 = lo - o1;    // class-0 ids before this chunk
+  for (int k = lo; k < hi; ++k) {
+    if (need[k]) list[tot0 + o1++] = k;
+    else list[o0++] = k;
+  }
+  if (t == 0) {
+    count[0] = tot0;
+    count[1] = tot1;
+  }
+}
+
+template <int ENV>
 __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
   const int G = 64 / n, NT = G * n;
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
-  const int sc = blockIdx.x * G + ls;
-  const bool valid = (lane < NT) && (sc < a.B);
-  CadmmLds L = cadmm_carve(smem, n);
+  const int cnt = a.scount[ENV];
+  if ((int)blockIdx.x * G >= cnt) return;  // block past the end of this class (uniform exit)
+  const int g = blockIdx.x * G + ls;
+  const bool valid = (lane < NT) && (g < cnt);
+  const int sc = valid ? a.slist[(ENV ? a.scount[0] : 0) + g] : 0;
+  CadmmLds L = cadmm_carve(smem, n, ENV);
   const int FXS = fx_stride(n);
   double* myf = L.fx + lane * FXS;
   double* fb = L.fbar + ls * N3;
@@ -148,9 +250,6 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   double* lam = nullptr;
   int iter = 0, qstat = ST_OPTIMAL;
   long long my_ipm = 0, my_qp = 0, my_rowit = 0;
-  EnvOut env;
-  env.collision = 0;
-  env.min_env_dist = 0.0;
   if (valid) {
     prm = prm_of(a, sc);
     const double* st = a.state + (size_t)sc * a.S;
@@ -166,22 +265,20 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     L.done[ls] = 1;
   }
   __syncthreads();
-  int nr = NBASE;
   if (valid) {
-    const double* st = a.state + (size_t)sc * a.S;
     lane_cadmm_static(P, prm, i);
-    const double* trees;
-    int nt;
-    unsigned emask;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
-    EnvRows E;
-    set_env_rows(P, E, S, emask, lhs, rhs);
-    env_to_lds(L.env, lane, E);
-    nr = rows_needed(P.emask);
+    if (ENV) {
+      const double* trees;
+      int nt;
+      unsigned emask;
+      forest_of(a, sc, &trees, &nt);
+      double lhs[DAT_NENV][3], rhs[DAT_NENV];
+      env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+      EnvRows E;
+      set_env_rows(P, E, S, emask, lhs, rhs);
+      env_to_lds(L.env, lane, E);
+    }
   }
-  nr = wave_max(nr);
   const LdsRef<QPShared> shr{L.sh, ls < G ? ls : 0};
   const EnvLds err{L.env, lane};
   const RtLds rtr{L.Rt, (ls < G ? ls : 0) * 9 * n + 9 * i};
@@ -193,7 +290,8 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ipm_solve<MODE_CADMM, 1, ENV ? DAT_MAXROW : NBASE>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
+                                                                    IPM_TOL);
       my_ipm += o.iters;
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
@@ -299,22 +397,9 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
       a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
     }
     a.qstatus[(size_t)sc * n + i] = qstat;
-    myred[0] = env.collision ? 1.0 : 0.0;
-    myred[1] = env.min_env_dist;
+    if (i == 0) a.iters[sc] = iter;
   }
-  __syncthreads();
-  if (valid && i == 0) {
-    a.iters[sc] = iter;
-    int coll = 0;
-    double md = prm[DAT_P_VISR];
-    for (int k = 0; k < n; ++k) {
-      coll |= L.red[(ls * n + k) * RDS] != 0.0;
-      md = fmin(md, L.red[(ls * n + k) * RDS + 1]);
-    }
-    a.col[sc] = (unsigned char)coll;
-    a.mind[sc] = md;
-  }
-  // work counters: one atomic per lane group
+  // work counters of this class: one atomic per wavefront
   unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
@@ -322,9 +407,9 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     rw += __shfl_xor(rw, off);
   }
   if (lane == 0) {
-    atomicAdd(a.counters, q);
-    atomicAdd(a.counters + 1, ip);
-    atomicAdd(a.counters + 2, rw);
+    atomicAdd(a.counters + 3 * ENV, q);
+    atomicAdd(a.counters + 3 * ENV + 1, ip);
+    atomicAdd(a.counters + 3 * ENV + 2, rw);
   }
 }
 
@@ -833,6 +918,8 @@ struct dat_handle {
   int P = 0, S = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t ek[3] = {nullptr, nullptr, nullptr};  // C-ADMM: after k_bucket, after k_cadmm<0>, after k_cadmm<1>
+  double class_ms[2] = {0.0, 0.0};                 // summed k_cadmm<k> time
   double* params = nullptr;
   int ppp = 0;
   bool have_params = false;
@@ -850,7 +937,8 @@ struct dat_handle {
   int *iters = nullptr, *qstatus = nullptr;
   double *mind = nullptr, *err = nullptr;
   unsigned char* col = nullptr;
-  unsigned long long* counters = nullptr;
+  unsigned long long* counters = nullptr;  // 6: [3k + .] of env class k (C-ADMM); [0..2] otherwise
+  int *need = nullptr, *slist = nullptr, *scount = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
   std::vector<void*> allocs;
@@ -916,6 +1004,9 @@ KArgs kargs(dat_handle* h) {
   a.col = h->col;
   a.err = h->err;
   a.counters = h->counters;
+  a.need = h->need;
+  a.slist = h->slist;
+  a.scount = h->scount;
   return a;
 }
 
@@ -939,7 +1030,13 @@ int launch_hl(dat_handle* h) {
   if (h->cfg.mode == DAT_MODE_CADMM) {
     int G = 64 / n;
     int blocks = (B + G - 1) / G;
-    hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(n), h->stream, a);
+    hipLaunchKernelGGL(k_env_class, dim3(blocks), dim3(64), 0, h->stream, a);
+    hipLaunchKernelGGL(k_bucket, dim3(1), dim3(1024), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
+    HIPCHK(hipEventRecord(h->ek[0], h->stream));
+    hipLaunchKernelGGL(k_cadmm<0>, dim3(blocks), dim3(64), cadmm_lds_bytes(n, false), h->stream, a);
+    HIPCHK(hipEventRecord(h->ek[1], h->stream));
+    hipLaunchKernelGGL(k_cadmm<1>, dim3(blocks), dim3(64), cadmm_lds_bytes(n, true), h->stream, a);
+    HIPCHK(hipEventRecord(h->ek[2], h->stream));
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
     int G = 64 / n;
@@ -962,6 +1059,13 @@ int finish_hl(dat_handle* h) {
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, h->e0, h->e1));
   h->hl_ms += ms;
+  if (h->cfg.mode == DAT_MODE_CADMM) {
+    for (int k = 0; k < 2; ++k) {
+      float mk = 0.f;
+      HIPCHK(hipEventElapsedTime(&mk, h->ek[k], h->ek[k + 1]));
+      h->class_ms[k] += mk;
+    }
+  }
   h->hl_steps += 1;
   return 0;
 }
@@ -1014,7 +1118,9 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   h->P = DAT_PARAM_SIZE(c.n);
   h->S = DAT_STATE_SIZE(c.n);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&h->e0) != hipSuccess || hipEventCreate(&h->e1) != hipSuccess) {
+      hipEventCreate(&h->e0) != hipSuccess || hipEventCreate(&h->e1) != hipSuccess ||
+      hipEventCreate(&h->ek[0]) != hipSuccess || hipEventCreate(&h->ek[1]) != hipSuccess ||
+      hipEventCreate(&h->ek[2]) != hipSuccess) {
     delete h;
     return fail("dat_create: stream/event creation failed");
   }
@@ -1028,9 +1134,12 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   rc |= dalloc(h, &h->qstatus, B * n);
   rc |= dalloc(h, &h->mind, B);
   rc |= dalloc(h, &h->col, B);
-  rc |= dalloc(h, &h->counters, 3);
+  rc |= dalloc(h, &h->counters, 6);
   if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
   if (c.mode == DAT_MODE_CADMM) {
+    rc |= dalloc(h, &h->need, B);
+    rc |= dalloc(h, &h->slist, B);
+    rc |= dalloc(h, &h->scount, 2);
     rc |= dalloc(h, &h->cf, B * n * N3);
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
@@ -1050,7 +1159,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     return fail(m);
   }
   // LDS budgets
-  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
+  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n, true) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
   if (lds > 160 * 1024) {
     dat_destroy(h);
     return fail("dat_create: LDS budget exceeded");
@@ -1067,6 +1176,8 @@ int dat_destroy(dat_handle* h) {
     if (p) (void)hipFree(p);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
+  for (hipEvent_t e : h->ek)
+    if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -1239,9 +1350,10 @@ int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, 
                      long long* hl_steps, double* hl_kernel_ms) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  unsigned long long c[3] = {0, 0, 0};
-  HIPCHK(hipMemcpyAsync(c, h->counters, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  unsigned long long c6[6] = {0, 0, 0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(c6, h->counters, sizeof(c6), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  const unsigned long long c[3] = {c6[0] + c6[3], c6[1] + c6[4], c6[2] + c6[5]};
   if (qp_solves) *qp_solves = (long long)c[0];
   if (ipm_iters) *ipm_iters = (long long)c[1];
   if (ipm_row_iters) *ipm_row_iters = (long long)c[2];
@@ -1250,10 +1362,27 @@ int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, 
   return 0;
 }
 
+int dat_get_class_counters(dat_handle* h, int env_class, long long* qp_solves, long long* ipm_iters,
+                           long long* ipm_row_iters, double* kernel_ms) {
+  if (!h) return fail("null handle");
+  if (h->cfg.mode != DAT_MODE_CADMM) return fail("dat_get_class_counters: C-ADMM handles only");
+  if (env_class < 0 || env_class > 1) return fail("dat_get_class_counters: env_class must be 0 or 1");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[3] = {0, 0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters + 3 * env_class, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (qp_solves) *qp_solves = (long long)c[0];
+  if (ipm_iters) *ipm_iters = (long long)c[1];
+  if (ipm_row_iters) *ipm_row_iters = (long long)c[2];
+  if (kernel_ms) *kernel_ms = h->class_ms[env_class];
+  return 0;
+}
+
 int dat_reset_counters(dat_handle* h) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  HIPCHK(hipMemsetAsync(h->counters, 0, 3 * sizeof(unsigned long long), h->stream));
+  HIPCHK(hipMemsetAsync(h->counters, 0, 6 * sizeof(unsigned long long), h->stream));
+  h->class_ms[0] = h->class_ms[1] = 0.0;
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
   h->hl_ms = 0.0;

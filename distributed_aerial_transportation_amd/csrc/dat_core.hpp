@@ -290,6 +290,28 @@ DAT_HD void trmtv6(const double* L, const double* v, double* o) {
     o[r] = s;
   }
 }
+// N = I + L' T L (packed) for a packed lower factor L with true diagonal and a packed symmetric T:
+// column c of T L, then the upper triangle of column c of L' (T L).
+DAT_HD void ltl_plus_identity(const double* L, const double* T, double* N) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    double col[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      double s = 0.0;
+#pragma unroll
+      for (int j = c; j < 6; ++j) s += T[sp6(k, j)] * L[sp6(j, c)];
+      col[k] = s;
+    }
+#pragma unroll
+    for (int r = 0; r <= c; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = r; k < 6; ++k) s += L[sp6(k, r)] * col[k];
+      N[sp6(r, c)] = s;
+    }
+  }
+}
 DAT_HD void chol6_solve(const double* L, double* b) {
 #pragma unroll
   for (int i = 0; i < 6; ++i) {

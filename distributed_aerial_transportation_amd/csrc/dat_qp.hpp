@@ -765,12 +765,14 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       okc = okc && inv3_spd(D, Dinv[k]);
     }
     if (!okc) break;
-    // M (packed) and, for CADMM / CENT, the LU factors of (I + M T); DD: the Cholesky factor of M
-    // parked in LU.  (Forming N = (I + M T)^-1 M explicitly would save registers but loses the
-    // accuracy the refinement needs once active rows make M huge.)
-    double Mm[21], LU[6][6];
-    int piv[6];
+    // M = Lm Lm' (Cholesky; M is SPD: C carries k_f, k_m > 0) and, for CADMM / CENT, the Cholesky
+    // factor Ln of the SPD matrix N = I + Lm' T Lm, so that (I + M T)^-1 M = Lm N^-1 Lm'.  N has
+    // every eigenvalue >= 1 however large active rows make M, so the solve stays well conditioned
+    // without a pivoted nonsymmetric LU (and needs 42 doubles of factors instead of 57 + pivots).
+    // DD: Lm alone (reciprocal diagonal, for chol6_solve).
+    double Lm[21], Ln[21];
     {
+      double Mm[21];
       // M = C + sum_l (z/s) a_l a_l' (u-space, packed), assembled in (dvl, dwl) coordinates
       {
         double Xv[6] = {0, 0, 0, 0, 0, 0}, Xw[6] = {0, 0, 0, 0, 0, 0};
@@ -808,11 +810,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           }
       }
       if (MODE == MODE_DD) {
-        double Lp[21];
-        if (!chol6(Mm, Lp)) break;
-#pragma unroll
-        for (int k = 0; k < 21; ++k) LU[k / 6][k % 6] = Lp[k];
+        if (!chol6(Mm, Lm)) break;
       } else {
+        if (!chol6_lower(Mm, Lm)) break;
         // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho)
         double T[21];
         if (MODE == MODE_CADMM) {
@@ -828,16 +828,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int k = 0; k < NB; ++k) add_UDUt(T, rt.get(k), Dinv[k], 1.0);
         }
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-          for (int c = 0; c < 6; ++c) {
-            double s = (r == c) ? 1.0 : 0.0;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) s += Mm[sp6(r, k)] * T[sp6(k, c)];
-            LU[r][c] = s;
-          }
-        if (!lu6(LU, piv)) break;
+        double Nn[21];
+        ltl_plus_identity(Lm, T, Nn);
+        if (!chol6(Nn, Ln)) break;
       }
     }
 
@@ -847,12 +840,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
                     double dyo[NB][3], double* dwo, double* duo) {
       double dyn[NB][3], dwn[6], dun[6];
       if (MODE == MODE_DD) {
-        double Lp[21];
-#pragma unroll
-        for (int k = 0; k < 21; ++k) Lp[k] = LU[k / 6][k % 6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) dun[r] = -Rfr[r] + (has_bu ? bu[r] : 0.0);
-        chol6_solve(Lp, dun);
+        chol6_solve(Lm, dun);
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double t[3], v[3];
@@ -891,9 +881,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
             yv[r] += g6[r] * irho;
           }
         }
-        double tau[6];
-        spmv6(Mm, yv, tau);
-        lu6_solve(LU, piv, tau);
+        // tau = (I + M T)^-1 M yv = Lm N^-1 Lm' yv
+        double tau[6], xs[6];
+        trmtv6(Lm, yv, xs);
+        chol6_solve(Ln, xs);
+        trmv6(Lm, xs, tau);
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double t[3], v[3];

@@ -98,6 +98,38 @@ def forest_start_states(n: int, batch: int, rng: np.random.Generator) -> np.ndar
     return np.stack(out)
 
 
+def forest_path_states(n: int, batch: int, rng: np.random.Generator, forests: list, scenario_forest: np.ndarray,
+                       x_range=(-2.0, 50.0), y_half=5.0, speed=(0.5, 1.0), clearance: float = 2.0) -> np.ndarray:
+    """Config C4 spread along the forest crossing of the reference run (example/rqp_example.py: the
+    payload starts at the origin, the forest spans x in [5, 55] and |vl| <= 1 m/s, so a 100 s run
+    is inside the forest for most of its steps): xl = (U(x_range), U(-y_half, y_half), terrain +
+    1.5), vl = (U(speed), 0, 0), rest attitude.  Positions whose xy distance to a tree axis is below
+    `clearance` are redrawn (no scenario starts inside a tree)."""
+    xl = np.empty((batch, 3))
+    sf = np.asarray(scenario_forest)
+    todo = np.arange(batch)
+    while todo.size:
+        xl[todo, 0] = rng.uniform(*x_range, todo.size)
+        xl[todo, 1] = rng.uniform(-y_half, y_half, todo.size)
+        bad = []
+        for f in np.unique(sf[todo]):
+            idx = todo[sf[todo] == f]
+            d = np.linalg.norm(xl[idx, None, :2] - forests[f].tree_pos[None, :, :2], axis=2).min(axis=1)
+            bad.append(idx[d < clearance])
+        todo = np.concatenate(bad) if bad else np.zeros(0, dtype=int)
+    for f in np.unique(sf):
+        idx = np.nonzero(sf == f)[0]
+        xl[idx, 2] = [forests[f].terrain_height(p) + 1.5 for p in xl[idx, :2]]
+    vx = rng.uniform(*speed, batch)
+    # rest attitude, zero rates: one packed template, then the per-scenario position and velocity
+    # (layout: csrc/dat_layout.h, DAT_S_XL = 12 n, DAT_S_VL = 12 n + 3)
+    tmpl = pack_state(rest_state(n))
+    out = np.tile(tmpl, (batch, 1))
+    out[:, 12 * n:12 * n + 3] = xl
+    out[:, 12 * n + 3] = vx
+    return out
+
+
 def params_block(n: int) -> np.ndarray:
     p, col, _ = rqp_setup(n)
     return pack_params(p, col)

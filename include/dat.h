@@ -115,6 +115,10 @@ int dat_closed_loop(dat_handle* h, int hl_steps);
  * of the high-level kernels [ms] (HIP events on the handle stream).  Any pointer may be NULL. */
 int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* ipm_row_iters,
                      long long* hl_steps, double* hl_kernel_ms);
+/* C-ADMM only: the same counters for one env class (0: scenarios whose agent QPs carry no env CBF
+ * row this step, 1: the others) and the summed device time of that class's k_cadmm launch [ms]. */
+int dat_get_class_counters(dat_handle* h, int env_class, long long* qp_solves, long long* ipm_iters,
+                           long long* ipm_row_iters, double* kernel_ms);
 int dat_reset_counters(dat_handle* h);
 int dat_synchronize(dat_handle* h);
 
