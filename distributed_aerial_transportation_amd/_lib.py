@@ -85,6 +85,7 @@ EXPORTS = {
     "dat_closed_loop": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_get_counters": (ctypes.c_int, [H, LL, LL, LL, LL, D]),
     "dat_get_class_counters": (ctypes.c_int, [H, ctypes.c_int, LL, LL, LL, D]),
+    "dat_get_class_occupancy": (ctypes.c_int, [H, ctypes.c_int, LL, LL]),
     "dat_reset_counters": (ctypes.c_int, [H]),
     "dat_synchronize": (ctypes.c_int, [H]),
     "dat_env_rows": (ctypes.c_int, [H, D, D, I, U8, D]),

@@ -194,12 +194,16 @@ class BatchedController:
                 "hl_kernel_ms": ms.value}
 
     def class_work(self, env_class: int) -> dict:
-        """C-ADMM only: work counters and summed kernel time of one env class (0: scenarios whose agent
-        QPs carry no env CBF row in the step, 1: the others) -- dat_get_class_counters."""
+        """C-ADMM only: work counters, summed kernel time and SIMD occupancy of one env class (0:
+        scenarios whose agent QPs carry no env CBF row in the step; 1, 2, 3: at most 2, 5, 10 env rows
+        per agent QP) -- dat_get_class_counters, dat_get_class_occupancy."""
         q, it, rw, ms = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_double()
         L.check(self._lib.dat_get_class_counters(self._h, int(env_class), ctypes.byref(q), ctypes.byref(it),
                                                  ctypes.byref(rw), ctypes.byref(ms)))
-        return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "kernel_ms": ms.value}
+        sl, wp = ctypes.c_longlong(), ctypes.c_longlong()
+        L.check(self._lib.dat_get_class_occupancy(self._h, int(env_class), ctypes.byref(sl), ctypes.byref(wp)))
+        return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "kernel_ms": ms.value,
+                "slot_ipm_iters": sl.value, "wave_admm_iters": wp.value}
 
     def reset_counters(self) -> None:
         L.check(self._lib.dat_reset_counters(self._h))

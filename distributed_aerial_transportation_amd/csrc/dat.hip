@@ -44,6 +44,16 @@ constexpr int NMAX = 16;        // largest team the kernels are compiled for
 constexpr int NMAX_DD = 8;      // DD master matrix is (6n)^2 in LDS
 constexpr int IPM_MAX_ITER = 50;
 constexpr double IPM_TOL = 1e-10;
+// C-ADMM env classes (cadmm_block<C>): 0 no env row, then the largest per-agent env-row count of the
+// scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
+constexpr int NCLS = 4;
+__host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 5 : DAT_NENV; }
+// k_bucket sort key: class x bin of the scenario's previous ADMM iteration count (1, 2, 3, >= 4),
+// so that scenarios sharing a wavefront tend to need the same number of ADMM passes
+constexpr int NIB = 4;
+constexpr int NKEY = NCLS * NIB;
+constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
+constexpr int DAT_NCOUNTERS = NCLS * CNT_STRIDE;
 
 struct KArgs {
   int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)
@@ -72,10 +82,10 @@ struct KArgs {
   unsigned char* col;
   double* err;
   unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
-                                 // (C-ADMM: [3k + .] per env class k of k_cadmm<ENV = k>)
-  int* need;                     // C-ADMM: per-scenario env class of the step (k_env_class)
-  int* slist;                    // C-ADMM: scenario ids, class 0 first, then class 1 (k_bucket)
-  int* scount;                   // C-ADMM: class sizes [2]
+                                 // (C-ADMM: [CNT_STRIDE k + .] per env class k, cadmm_block<k>)
+  int* need;                     // C-ADMM: per-scenario sort key of the step (k_env_class)
+  int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
+  int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)
@@ -102,38 +112,41 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 // A control step runs as four launches:
 //   k_env_class   one lane per agent: env CBF rows of the step (they depend on the state only, so
 //                 they are fixed for the whole ADMM loop, control/rqp_cadmm.py:305), per-scenario
-//                 env class (1 if any agent's QP carries an env row), collision, min env distance;
-//   k_bucket      stable partition of the scenario ids by class;
-//   k_cadmm<0>    the scenarios without env rows: 3 row slots, no env image in LDS, so the IPM's
-//                 register budget and the workgroup's LDS are sized for the common case;
-//   k_cadmm<1>    the scenarios with env rows (13 row slots, env image in LDS).
+//                 env class (the largest env-row count among its agents' QPs: 0, <= 2, <= 5,
+//                 <= 10), collision, min env distance, and a sort key (class, previous step's
+//                 ADMM iteration count);
+//   k_bucket      stable counting sort of the scenario ids by key;
+//   k_cadmm0      class 0 (3 row slots, no env image in LDS), on a side stream, concurrently with
+//   k_cadmm_env   classes 1..3 (3 + {2, 5, 10} row slots: the IPM's register footprint follows
+//                 the rows the class needs) in one launch, so class tails overlap.
+// Sorting by the previous ADMM iteration count groups scenarios that need a similar number of
+// ADMM passes into one wavefront (a wavefront runs until its slowest scenario stops).
 // Each scenario's arithmetic does not depend on the scenarios it shares a wavefront with (padding
 // rows add exact zeros), so the regrouping does not change any result.
 //
 // LDS layout of one 64-lane block (G = floor(64/n) scenarios).  Per-lane records use an odd
 // stride in doubles so that the 32 lanes of a ds_read_b64 group fall on distinct bank pairs.
-//   fx   NT x FXS  agent copies f^(i) (FXS = 3n rounded up to odd)    fbar G x 3n  consensus mean
+//   fbar G x 3n    consensus mean
 //   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x RDS (9)  per-lane exchange slots
 //   sh   G x QPShared (u-maps, packed Hessians, base rows, K)
-//   env  EnvLds image (structure of arrays over the 64 lanes; class-1 kernel only)   done G ints
+//   env  EnvLds image (structure of arrays over the 64 lanes; env classes only)   done G ints
+// (n = 6: 19.6 KB without, 39.6 KB with the env image, so four wavefronts fit a CU's 160 KB.)
 constexpr int RDS = 9;
-__host__ __device__ inline int fx_stride(int n) { return (3 * n) | 1; }
 struct CadmmLds {
-  double *fx, *fbar, *Rt, *red;
+  double *fbar, *Rt, *red;
   QPShared* sh;
   double* env;
   int* done;
 };
 __host__ __device__ inline size_t cadmm_lds_bytes(int n, bool env) {
-  const int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * fx_stride(n) + (size_t)G * 3 * n + (size_t)G * 9 * n + 64 * RDS) +
+  const int G = 64 / n;
+  return sizeof(double) * ((size_t)G * 3 * n + (size_t)G * 9 * n + 64 * RDS) +
          sizeof(QPShared) * (size_t)G + (env ? sizeof(double) * ENV_LDS_DOUBLES : 0) + sizeof(int) * 64;
 }
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, bool env) {
-  const int G = 64 / n, NT = G * n;
+  const int G = 64 / n;
   CadmmLds L;
-  L.fx = smem;
-  L.fbar = L.fx + NT * fx_stride(n);
+  L.fbar = smem;
   L.Rt = L.fbar + G * 3 * n;
   L.red = L.Rt + G * 9 * n;
   L.sh = (QPShared*)(L.red + 64 * RDS);
@@ -142,17 +155,24 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, bool env) {
   return L;
 }
 
-// the QP must carry env rows: a nonzero row, or an all-zero row with a positive right-hand side
-// (0 >= rhs > 0 makes the reference's QP infeasible; set_env_rows flags it)
-__device__ inline bool env_rows_needed(unsigned emask, const double lhs[DAT_NENV][3], const double rhs[DAT_NENV]) {
+// env class of one agent QP: 0 if it carries no env row, otherwise the smallest class whose slots
+// hold the rows set_env_rows keeps (nonzero rows, compacted).  An all-zero row with a positive
+// right-hand side (0 >= rhs > 0: the reference's QP is infeasible, set_env_rows flags it) also
+// needs an env class.
+__device__ inline int env_class_of(unsigned emask, const double lhs[DAT_NENV][3], const double rhs[DAT_NENV]) {
   bool need = false;
+  int k = 0;
 #pragma unroll
   for (int j = 0; j < DAT_NENV; ++j) {
     const bool on = (emask >> j) & 1u;
     const bool zero = lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0;
     need = need || (on && (!zero || rhs[j] > 0.0));
+    k += (on && !zero) ? 1 : 0;
   }
-  return need;
+  if (!need) return 0;
+  int c = 1;
+  while (c < NCLS - 1 && k > class_env_rows(c)) ++c;
+  return c;
 }
 
 __global__ __launch_bounds__(64) void k_env_class(KArgs a) {
@@ -173,7 +193,7 @@ __global__ __launch_bounds__(64) void k_env_class(KArgs a) {
     forest_of(a, sc, &trees, &nt);
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
     EnvOut e = env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
-    need = env_rows_needed(emask, lhs, rhs) ? 1 : 0;
+    need = env_class_of(emask, lhs, rhs);
     col = e.collision;
     dist = e.min_env_dist;
   }
@@ -182,64 +202,106 @@ __global__ __launch_bounds__(64) void k_env_class(KArgs a) {
   md[lane] = dist;
   __syncthreads();
   if (valid && i == 0) {
-    int any = 0, c = 0;
+    int cls = 0, c = 0;
     double m = prm_of(a, sc)[DAT_P_VISR];
     for (int k = 0; k < n; ++k) {
-      any |= nd[ls * n + k];
+      cls = max(cls, nd[ls * n + k]);
       c |= cl[ls * n + k];
       m = fmin(m, md[ls * n + k]);
     }
-    a.need[sc] = any;
+    const int bin = min(max(a.iters[sc] - 1, 0), NIB - 1);  // previous step's ADMM iterations
+    a.need[sc] = cls * NIB + bin;
     a.col[sc] = (unsigned char)c;
     a.mind[sc] = m;
   }
 }
 
-// Stable partition of the scenario ids by need[]: list = [class 0 ..., class 1 ...], count[k] =
-// size of class k.  One 1024-thread workgroup; each thread owns a contiguous chunk.
-__global__ __launch_bounds__(1024) void k_bucket(int B, const int* need, int* list, int* count) {
-  __shared__ int s[1024];
+// Stable counting sort of the scenario ids by key (need[] in [0, NKEY)): list holds the ids of key
+// 0, then key 1, ...; count[c] / count[NCLS + c] = size / start of env class c (keys c NIB ..
+// c NIB + NIB - 1).  One BUCKET_T-thread workgroup; each thread owns a contiguous chunk of ids.
+// Grouping only changes which scenarios share a wavefront, never a scenario's arithmetic.
+constexpr int BUCKET_T = 512;
+__global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int* list, int* count) {
+  __shared__ int s[NKEY][BUCKET_T + 1];
+  __shared__ int tot[NKEY];
   const int t = threadIdx.x;
-  const int chunk = (B + 1023) / 1024;
+  const int chunk = (B + BUCKET_T - 1) / BUCKET_T;
   const int lo = min(B, t * chunk), hi = min(B, lo + chunk);
-  int c1 = 0;
-  for (int k = lo; k < hi; ++k) c1 += need[k] != 0;
-  s[t] = c1;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int v = t >= off ? s[t - off] : 0;
-    __syncthreads();
-    s[t] += v;
-    __syncthreads();
+  int c[NKEY];
+#pragma unroll
+  for (int k = 0; k < NKEY; ++k) c[k] = 0;
+  for (int q = lo; q < hi; ++q) {
+    const int key = min(max(need[q], 0), NKEY - 1);
+#pragma unroll
+    for (int k = 0; k < NKEY; ++k) c[k] += key == k;
   }
-  const int tot1 = s[1023], tot0 = B - tot1;
-  int o1 = s[t] - c1;  // class-1 ids before this chunk
-  int o0 = lo - o1;    // class-0 ids before this chunk
-  for (int k = lo; k < hi; ++k) {
-    if (need[k]) list[tot0 + o1++] = k;
-    else list[o0++] = k;
+#pragma unroll
+  for (int k = 0; k < NKEY; ++k) s[k][t + 1] = c[k];
+  if (t < NKEY) s[t][0] = 0;
+  __syncthreads();
+  // exclusive scan over threads: wavefront w scans keys w, w + BUCKET_T / 64, ...
+  for (int k = t / 64; k < NKEY; k += BUCKET_T / 64) {
+    const int l = t % 64;
+    int run = 0;
+    for (int base = 0; base < BUCKET_T; base += 64) {  // inclusive prefix of s[k][1 ..] in 64-wide tiles
+      int v = s[k][base + l + 1];
+      for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(v, off);
+        if (l >= off) v += u;
+      }
+      s[k][base + l + 1] = v + run;
+      run += __shfl(v, 63);
+    }
+    if (l == 0) tot[k] = run;
+  }
+  __syncthreads();
+  int off[NKEY], start = 0;
+#pragma unroll
+  for (int k = 0; k < NKEY; ++k) {
+    off[k] = start + s[k][t];
+    start += tot[k];
+  }
+  for (int q = lo; q < hi; ++q) {
+    const int key = min(max(need[q], 0), NKEY - 1);
+    int pos = 0;
+#pragma unroll
+    for (int k = 0; k < NKEY; ++k)
+      if (key == k) pos = off[k]++;
+    list[pos] = q;
   }
   if (t == 0) {
-    count[0] = tot0;
-    count[1] = tot1;
+    int st = 0;
+    for (int cl = 0; cl < NCLS; ++cl) {
+      int sz = 0;
+      for (int b = 0; b < NIB; ++b) sz += tot[cl * NIB + b];
+      count[cl] = sz;
+      count[NCLS + cl] = st;
+      st += sz;
+    }
   }
 }
 
-template <int ENV>
-__global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
+// One 64-lane block of env class CLS; blk = the block's index within the class.
+template <int CLS>
+__device__ __forceinline__ void cadmm_block(const KArgs& a, int blk) {
+  constexpr bool ENV = CLS > 0;
+  constexpr int NR = NBASE + class_env_rows(CLS);
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
   const int G = 64 / n, NT = G * n;
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
-  const int cnt = a.scount[ENV];
-  if ((int)blockIdx.x * G >= cnt) return;  // block past the end of this class (uniform exit)
-  const int g = blockIdx.x * G + ls;
+  const int cnt = a.scount[CLS];
+  if (blk * G >= cnt) return;  // block past the end of this class (uniform exit)
+  const int g = blk * G + ls;
   const bool valid = (lane < NT) && (g < cnt);
-  const int sc = valid ? a.slist[(ENV ? a.scount[0] : 0) + g] : 0;
+  const int sc = valid ? a.slist[a.scount[NCLS + CLS] + g] : 0;
   CadmmLds L = cadmm_carve(smem, n, ENV);
-  const int FXS = fx_stride(n);
-  double* myf = L.fx + lane * FXS;
+  // agent copies f^(i) live in the persistent warm-state array itself (HBM / L2): they are read by
+  // the other lanes of the scenario only in the consensus step, and keeping them out of LDS lets
+  // four env-class wavefronts share a CU
+  double* const cfs = a.cf + (size_t)sc * n * N3;  // the scenario's n copies
+  double* myf = cfs + i * N3;
   double* fb = L.fbar + ls * N3;
   double* rts = L.Rt + ls * 9 * n;
   double* myred = L.red + lane * RDS;
@@ -250,11 +312,11 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   double* lam = nullptr;
   int iter = 0, qstat = ST_OPTIMAL;
   long long my_ipm = 0, my_qp = 0, my_rowit = 0;
+  long long wv_slot = 0, wv_pass = 0;  // wave-level: sum of (max lane IPM iterations) per pass, passes
   if (valid) {
     prm = prm_of(a, sc);
     const double* st = a.state + (size_t)sc * a.S;
     make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + 9 * i);
-    for (int c = 0; c < N3; ++c) myf[c] = a.cf[((size_t)sc * n + i) * N3 + c];
     for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
     lam = a.clam + ((size_t)sc * n + i) * N3;
     if (i == 0) {
@@ -287,12 +349,13 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   double rho = a.rho0;
   for (;;) {
     const bool active = valid && !L.done[ls];
+    int it_lane = 0;
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_CADMM, 1, ENV ? DAT_MAXROW : NBASE>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
-                                                                    IPM_TOL);
+      IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
       my_ipm += o.iters;
+      it_lane = o.iters;
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
@@ -308,6 +371,9 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
         for (int c = 0; c < N3; ++c) myf[c] = prm[DAT_P_FEQ(n) + c];
       }  // otherwise hold the previous solution (control/rqp_cadmm.py:496-499)
     }
+    for (int off = 32; off > 0; off >>= 1) it_lane = max(it_lane, __shfl_xor(it_lane, off));
+    wv_slot += it_lane;
+    ++wv_pass;
     __syncthreads();
     if (active) {
       ++iter;
@@ -315,7 +381,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
       // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
       for (int c = 0; c < 3; ++c) {
         double s = 0.0;
-        for (int k = 0; k < n; ++k) s += L.fx[(ls * n + k) * FXS + 3 * i + c];
+        for (int k = 0; k < n; ++k) s += cfs[k * N3 + 3 * i + c];
         myred[c] = s / n;
       }
     }
@@ -345,7 +411,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
         // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
         for (int k = 0; k < n; ++k) {
           if (k == i) continue;
-          const double* fk = L.fx + (ls * n + k) * FXS + 3 * k;  // f_app_k = agent k's own block
+          const double* fk = cfs + k * N3 + 3 * k;  // f_app_k = agent k's own block
           double m3[3];
           mv3(rts + 9 * k, fk, m3);
           for (int c = 0; c < 3; ++c) { F[c] -= fk[c]; M[c] -= m3[c]; }
@@ -391,7 +457,6 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   }
   // epilogue
   if (valid) {
-    for (int c = 0; c < N3; ++c) a.cf[((size_t)sc * n + i) * N3 + c] = myf[c];
     for (int c = 0; c < 3; ++c) {
       a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
       a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
@@ -407,10 +472,35 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
     rw += __shfl_xor(rw, off);
   }
   if (lane == 0) {
-    atomicAdd(a.counters + 3 * ENV, q);
-    atomicAdd(a.counters + 3 * ENV + 1, ip);
-    atomicAdd(a.counters + 3 * ENV + 2, rw);
+    unsigned long long* cc = a.counters + CNT_STRIDE * CLS;
+    atomicAdd(cc, q);
+    atomicAdd(cc + 1, ip);
+    atomicAdd(cc + 2, rw);
+    atomicAdd(cc + 3, (unsigned long long)(wv_slot * NT));
+    atomicAdd(cc + 4, (unsigned long long)(wv_pass * G));
   }
+}
+
+// class 0 (no env rows, small LDS footprint): one block per G scenarios of the class
+__global__ __launch_bounds__(64) void k_cadmm0(KArgs a) { cadmm_block<0>(a, blockIdx.x); }
+
+// classes 1..3 in one launch, so that the tail of one class overlaps the others; the blocks of the
+// class with the most rows (the longest-running) come first in dispatch order
+__global__ __launch_bounds__(64) void k_cadmm_env(KArgs a) {
+  const int G = 64 / a.n;
+  int b = blockIdx.x;
+  const int n3 = (a.scount[3] + G - 1) / G;
+  if (b < n3) {
+    cadmm_block<3>(a, b);
+    return;
+  }
+  b -= n3;
+  const int n2 = (a.scount[2] + G - 1) / G;
+  if (b < n2) {
+    cadmm_block<2>(a, b);
+    return;
+  }
+  cadmm_block<1>(a, b - n2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -918,8 +1008,9 @@ struct dat_handle {
   int P = 0, S = 0;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipEvent_t ek[3] = {nullptr, nullptr, nullptr};  // C-ADMM: after k_bucket, after k_cadmm<0>, after k_cadmm<1>
-  double class_ms[2] = {0.0, 0.0};                 // summed k_cadmm<k> time
+  hipStream_t side = nullptr;    // C-ADMM: class-0 launches run here, concurrently with the env classes
+  hipEvent_t ek[3] = {};         // C-ADMM: after k_bucket, after k_cadmm0 (side), after k_cadmm_env
+  double class_ms[2] = {};       // summed device time of k_cadmm0, k_cadmm_env
   double* params = nullptr;
   int ppp = 0;
   bool have_params = false;
@@ -937,7 +1028,7 @@ struct dat_handle {
   int *iters = nullptr, *qstatus = nullptr;
   double *mind = nullptr, *err = nullptr;
   unsigned char* col = nullptr;
-  unsigned long long* counters = nullptr;  // 6: [3k + .] of env class k (C-ADMM); [0..2] otherwise
+  unsigned long long* counters = nullptr;  // DAT_NCOUNTERS: [CNT_STRIDE k + .] of env class k (C-ADMM); [0..2] otherwise
   int *need = nullptr, *slist = nullptr, *scount = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
@@ -1031,12 +1122,15 @@ int launch_hl(dat_handle* h) {
     int G = 64 / n;
     int blocks = (B + G - 1) / G;
     hipLaunchKernelGGL(k_env_class, dim3(blocks), dim3(64), 0, h->stream, a);
-    hipLaunchKernelGGL(k_bucket, dim3(1), dim3(1024), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
+    hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
+    // class 0 on the side stream, concurrently with the env classes on the handle stream
     HIPCHK(hipEventRecord(h->ek[0], h->stream));
-    hipLaunchKernelGGL(k_cadmm<0>, dim3(blocks), dim3(64), cadmm_lds_bytes(n, false), h->stream, a);
-    HIPCHK(hipEventRecord(h->ek[1], h->stream));
-    hipLaunchKernelGGL(k_cadmm<1>, dim3(blocks), dim3(64), cadmm_lds_bytes(n, true), h->stream, a);
+    HIPCHK(hipStreamWaitEvent(h->side, h->ek[0], 0));
+    hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(n, false), h->side, a);
+    HIPCHK(hipEventRecord(h->ek[1], h->side));
+    hipLaunchKernelGGL(k_cadmm_env, dim3(blocks + NCLS), dim3(64), cadmm_lds_bytes(n, true), h->stream, a);
     HIPCHK(hipEventRecord(h->ek[2], h->stream));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ek[1], 0));
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
     int G = 64 / n;
@@ -1060,11 +1154,11 @@ int finish_hl(dat_handle* h) {
   HIPCHK(hipEventElapsedTime(&ms, h->e0, h->e1));
   h->hl_ms += ms;
   if (h->cfg.mode == DAT_MODE_CADMM) {
-    for (int k = 0; k < 2; ++k) {
-      float mk = 0.f;
-      HIPCHK(hipEventElapsedTime(&mk, h->ek[k], h->ek[k + 1]));
-      h->class_ms[k] += mk;
-    }
+    float m0 = 0.f, m1 = 0.f;
+    HIPCHK(hipEventElapsedTime(&m0, h->ek[0], h->ek[1]));
+    HIPCHK(hipEventElapsedTime(&m1, h->ek[0], h->ek[2]));
+    h->class_ms[0] += m0;
+    h->class_ms[1] += m1;
   }
   h->hl_steps += 1;
   return 0;
@@ -1118,9 +1212,13 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   h->P = DAT_PARAM_SIZE(c.n);
   h->S = DAT_STATE_SIZE(c.n);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&h->e0) != hipSuccess || hipEventCreate(&h->e1) != hipSuccess ||
-      hipEventCreate(&h->ek[0]) != hipSuccess || hipEventCreate(&h->ek[1]) != hipSuccess ||
-      hipEventCreate(&h->ek[2]) != hipSuccess) {
+      [&] {
+        for (auto& e : h->ek)
+          if (hipEventCreate(&e) != hipSuccess) return true;
+        return false;
+      }()) {
     delete h;
     return fail("dat_create: stream/event creation failed");
   }
@@ -1134,12 +1232,12 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   rc |= dalloc(h, &h->qstatus, B * n);
   rc |= dalloc(h, &h->mind, B);
   rc |= dalloc(h, &h->col, B);
-  rc |= dalloc(h, &h->counters, 6);
+  rc |= dalloc(h, &h->counters, DAT_NCOUNTERS);
   if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
   if (c.mode == DAT_MODE_CADMM) {
     rc |= dalloc(h, &h->need, B);
     rc |= dalloc(h, &h->slist, B);
-    rc |= dalloc(h, &h->scount, 2);
+    rc |= dalloc(h, &h->scount, 2 * NCLS);
     rc |= dalloc(h, &h->cf, B * n * N3);
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
@@ -1178,7 +1276,9 @@ int dat_destroy(dat_handle* h) {
   if (h->e1) (void)hipEventDestroy(h->e1);
   for (hipEvent_t e : h->ek)
     if (e) (void)hipEventDestroy(e);
+  if (h->side) (void)hipStreamSynchronize(h->side);
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->side) (void)hipStreamDestroy(h->side);
   delete h;
   return 0;
 }
@@ -1350,10 +1450,13 @@ int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, 
                      long long* hl_steps, double* hl_kernel_ms) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  unsigned long long c6[6] = {0, 0, 0, 0, 0, 0};
-  HIPCHK(hipMemcpyAsync(c6, h->counters, sizeof(c6), hipMemcpyDeviceToHost, h->stream));
+  unsigned long long cc[DAT_NCOUNTERS] = {};
+  HIPCHK(hipMemcpyAsync(cc, h->counters, sizeof(cc), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  const unsigned long long c[3] = {c6[0] + c6[3], c6[1] + c6[4], c6[2] + c6[5]};
+  unsigned long long c[3] = {cc[0], cc[1], cc[2]};
+  if (h->cfg.mode == DAT_MODE_CADMM)
+    for (int k = 1; k < NCLS; ++k)
+      for (int j = 0; j < 3; ++j) c[j] += cc[CNT_STRIDE * k + j];
   if (qp_solves) *qp_solves = (long long)c[0];
   if (ipm_iters) *ipm_iters = (long long)c[1];
   if (ipm_row_iters) *ipm_row_iters = (long long)c[2];
@@ -1366,23 +1469,36 @@ int dat_get_class_counters(dat_handle* h, int env_class, long long* qp_solves, l
                            long long* ipm_row_iters, double* kernel_ms) {
   if (!h) return fail("null handle");
   if (h->cfg.mode != DAT_MODE_CADMM) return fail("dat_get_class_counters: C-ADMM handles only");
-  if (env_class < 0 || env_class > 1) return fail("dat_get_class_counters: env_class must be 0 or 1");
+  if (env_class < 0 || env_class >= NCLS) return fail("dat_get_class_counters: env_class must be in [0, 4)");
   HIPCHK(hipSetDevice(h->cfg.device));
   unsigned long long c[3] = {0, 0, 0};
-  HIPCHK(hipMemcpyAsync(c, h->counters + 3 * env_class, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_STRIDE * env_class, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (qp_solves) *qp_solves = (long long)c[0];
   if (ipm_iters) *ipm_iters = (long long)c[1];
   if (ipm_row_iters) *ipm_row_iters = (long long)c[2];
-  if (kernel_ms) *kernel_ms = h->class_ms[env_class];
+  if (kernel_ms) *kernel_ms = h->class_ms[env_class == 0 ? 0 : 1];
+  return 0;
+}
+
+int dat_get_class_occupancy(dat_handle* h, int env_class, long long* slot_ipm_iters, long long* wave_admm_iters) {
+  if (!h) return fail("null handle");
+  if (h->cfg.mode != DAT_MODE_CADMM) return fail("dat_get_class_occupancy: C-ADMM handles only");
+  if (env_class < 0 || env_class >= NCLS) return fail("dat_get_class_occupancy: env_class must be in [0, 4)");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_STRIDE * env_class + 3, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (slot_ipm_iters) *slot_ipm_iters = (long long)c[0];
+  if (wave_admm_iters) *wave_admm_iters = (long long)c[1];
   return 0;
 }
 
 int dat_reset_counters(dat_handle* h) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
-  HIPCHK(hipMemsetAsync(h->counters, 0, 6 * sizeof(unsigned long long), h->stream));
-  h->class_ms[0] = h->class_ms[1] = 0.0;
+  HIPCHK(hipMemsetAsync(h->counters, 0, DAT_NCOUNTERS * sizeof(unsigned long long), h->stream));
+  for (double& m : h->class_ms) m = 0.0;
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
   h->hl_ms = 0.0;
