@@ -186,13 +186,12 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     launch_ms = hl_ms_rank0 / max(hl_steps, 1)
     # roofline of the dominant kernel, rank 0's own launches: algorithmic flops of one launch / its
-    # average duration (HIP events on the handle's stream).  C-ADMM runs one k_cadmm launch per env
-    # class (k_cadmm<0>: no env rows, k_cadmm<1..3>: up to 2 / 5 / 10 env rows per agent QP); the
-    # dominant one is the longest.
+    # average duration (HIP events on the handle's stream).  C-ADMM: k_cadmm (env classes 0..3: no
+    # env rows, up to 2 / 5 / 10 env rows per agent QP, all drained by one persistent launch).
     kernel, k_ipm, k_row, k_ms, classes = "k_cadmm", ipm, row_it, hl_ms, None
     if args.mode == "cadmm":
-        # two launches: k_cadmm0 (env class 0) and k_cadmm_env (classes 1..3, one launch)
-        classes, launches = {}, {"k_cadmm0": [0, 0, 0.0], "k_cadmm_env": [0, 0, 0.0]}
+        # one persistent k_cadmm launch per control step drains the four env classes
+        classes = {}
         for k in range(4):
             w = eng.class_work(k)
             classes[f"class{k}"] = {"qp_solves": w["qp_solves"], "ipm_iters": w["ipm_iters"],
@@ -200,14 +199,7 @@ def main():
                                     # useful lane-iterations / lane-iterations the wavefronts ran
                                     "ipm_lane_utilisation": w["ipm_iters"] / max(w["slot_ipm_iters"], 1),
                                     "admm_slot_utilisation": w["qp_solves"] / n / max(w["wave_admm_iters"], 1)}
-            L = launches["k_cadmm0" if k == 0 else "k_cadmm_env"]
-            L[0] += w["ipm_iters"]
-            L[1] += w["ipm_row_iters"]
-            L[2] = w["kernel_ms"]
-        for name, (li, lr, lms) in launches.items():
-            classes[name] = {"ms_per_launch": lms / max(hl_steps, 1)}
-            if lms >= (k_ms if kernel != "k_cadmm" else 0.0):
-                kernel, k_ipm, k_row, k_ms = name, li, lr, lms
+            k_ms = w["kernel_ms"]
     kernel_ms = k_ms / max(hl_steps, 1)
     flops_launch = (FLOPS_FIXED * k_ipm + FLOPS_PER_ROW * k_row) / max(hl_steps, 1)
     achieved_tflops = flops_launch / max(kernel_ms * 1e-3, 1e-12) / 1e12

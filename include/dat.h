@@ -115,10 +115,9 @@ int dat_closed_loop(dat_handle* h, int hl_steps);
  * of the high-level kernels [ms] (HIP events on the handle stream).  Any pointer may be NULL. */
 int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* ipm_row_iters,
                      long long* hl_steps, double* hl_kernel_ms);
-/* C-ADMM only: the same counters for one env class and the summed device time of the launch that
- * runs the class [ms].  env_class in [0, 4): scenarios whose agent QPs carry no env CBF row this
- * step (0), or at most 2 (1), 5 (2), 10 (3) env rows per agent QP.  Class 0 runs in its own launch
- * (k_cadmm0); classes 1..3 share one launch (k_cadmm_env), whose time all three report. */
+/* C-ADMM only: the same counters for one env class and the summed device time of k_cadmm [ms]
+ * (one persistent launch drains every class).  env_class in [0, 4): scenarios whose agent QPs carry
+ * no env CBF row this step (0), or at most 2 (1), 5 (2), 10 (3) env rows per agent QP. */
 int dat_get_class_counters(dat_handle* h, int env_class, long long* qp_solves, long long* ipm_iters,
                            long long* ipm_row_iters, double* kernel_ms);
 /* C-ADMM only, SIMD occupancy of one env class: slot_ipm_iters = sum over wavefront ADMM passes of
