@@ -55,15 +55,73 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=65536, help="scenarios per GPU")
-    ap.add_argument("--n", type=int, default=6)
-    ap.add_argument("--mode", default="cadmm")
+    ap.add_argument("--batch", type=int, default=None, help="scenarios per GPU (C4: 65536)")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--mode", default=None)
     ap.add_argument("--forests", type=int, default=64)
     ap.add_argument("--start", choices=["path", "edge"], default="path",
                     help="path: scenarios spread along the forest crossing (default); edge: all at the forest edge")
+    ap.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default="C4",
+                    help="SURVEY.md 8(d) workload; C4 (default) is the headline closed loop, C2/C3/C5 are the "
+                         "QP-level configs (n, mode, batch and parameters follow the config unless given)")
+    ap.add_argument("--fixed-work", action="store_true",
+                    help="C2/C5 mode (ii): tol 0, 25 ADMM iterations (test/control/test_rqpcontrollers.py:106-110)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
-    return ap.parse_args()
+    args = ap.parse_args()
+    n, mode, batch = QP_CONFIGS.get(args.config, (6, "cadmm", 65536))
+    args.n = n if args.n is None else args.n
+    args.mode = mode if args.mode is None else args.mode
+    args.batch = batch if args.batch is None else args.batch
+    return args
+
+
+# (n, controller, scenarios per GPU) of the QP-level configs
+QP_CONFIGS = {"C2": (3, "cadmm", 1024), "C3": (6, "dd", 16384), "C5": (16, "cadmm", 32768)}
+ACC_POOL = 8  # distinct acc_des draws cycled over the timed steps
+
+
+def qp_level_inputs(cfg: str, n: int, batch: int, rng: np.random.Generator):
+    """C2/C3/C5 inputs: perturbed rest states (scenarios.perturbed_states), acc_des ~ U(-5, 5)^6
+    (test/control/test_rqpcontrollers.py:117-118); C3 adds per-scenario payload mass / inertia."""
+    from distributed_aerial_transportation_amd import scenarios
+
+    states = scenarios.perturbed_states(n, batch, rng)
+    accs = [rng.uniform(-0.5, 0.5, (batch, 6)) * 10.0 for _ in range(ACC_POOL)]
+    if cfg == "C3":
+        return states, accs, scenarios.randomized_params(n, batch, rng), True
+    return states, accs, scenarios.params_block(n), False
+
+
+def cpu_baseline_qp(cfg: str, n: int, mode: str, budget_s: float, fixed_work: bool):
+    """Oracle (numpy) controller on a bounded sample of the same QP-level workload, one core."""
+    from distributed_aerial_transportation_amd import scenarios
+    from distributed_aerial_transportation_amd.system import RQPState
+    from oracle import controllers as oc
+    from oracle import model as om
+    from oracle import scenarios as osc
+
+    rng = np.random.default_rng(321)
+    solves, steps, t0 = 0, 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        x = scenarios.perturbed_states(n, 1, rng)[0]
+        acc = rng.uniform(-0.5, 0.5, 6) * 10.0
+        m, J, ml, Jl, r = osc.geometry(n)
+        if cfg == "C3":
+            ml, Jl = rng.uniform(0.15, 0.30), Jl * np.diag(rng.uniform(0.8, 1.2, 3))
+        p = om.Params(m, J, ml, Jl, r)
+        ctl = (oc.DD if mode == "dd" else oc.CADMM)(p, osc.col_radius(n))
+        if fixed_work and mode == "cadmm":
+            ctl.set_force_err_tolerance(0.0, False)
+            ctl.set_max_iter(25)
+        s = RQPState.unpack(x, n)
+        _, st = ctl.control(om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False), (acc[:3], acc[3:]))
+        solves += st.iter * n
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
+            "sample": f"oracle {mode} n={n} (numpy dense IPM), {steps} cold control steps of {cfg} inputs, "
+                      f"{solves} agent QPs in {dt:.1f} s"}
 
 
 def cpu_baseline(n: int, budget_s: float, start: str = "path"):
@@ -134,6 +192,8 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
     from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
 
+    if args.config != "C4":
+        return qp_level(args, dist, rank, world, local)
     n, B = args.n, args.batch
     scen_forest, seed = shard(rank, B, args.forests)
     rng = np.random.default_rng(seed)
@@ -232,6 +292,91 @@ def main():
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def qp_level(args, dist, rank: int, world: int, local: int):
+    """C2 / C3 / C5: one step = one batched control step of every scenario from HBM-resident states
+    (no rollout, no env).  acc_des cycles through ACC_POOL pre-drawn arrays; its host-to-device copy
+    (48 B per scenario) is inside the timed region.  Warm state (f, f_bar, lambda / lambda_F,M)
+    persists across steps as in the reference controller objects."""
+    from distributed_aerial_transportation_amd import BatchedController, _lib as L
+
+    n, B, cfg = args.n, args.batch, args.config
+    rng = np.random.default_rng(2000 + rank)
+    states, accs, params, per_scen = qp_level_inputs(cfg, n, B, rng)
+    eng = BatchedController(args.mode, n, B, params, per_scenario_params=per_scen,
+                            device=local if world > 1 else 0)
+    if args.fixed_work:
+        eng.set_force_err_tolerance(0.0, False)
+        eng.set_max_iter(25)
+    eng.set_state(states)
+    accs = [L.f64(a) for a in accs]
+    lib, h = eng._lib, eng._h
+
+    def step(k):
+        L.check(lib.dat_control_step(h, None, L.ptr(accs[k % ACC_POOL]), None, None, None, None, None, None))
+
+    for k in range(args.warmup):
+        step(k)
+    eng.synchronize()
+    eng.reset_counters()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    w = eng.work()
+    res = eng.control(None, L.f64(accs[0]))  # metrics only (outside the timed region)
+    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
+    tot = np.array([w["qp_solves"], w["ipm_iters"], w["hl_kernel_ms"], elapsed, w["ipm_row_iters"]])
+    if dist is not None:
+        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, f"cuda:{local}")
+        qps, ipm, rows, elapsed = float(sums[0]), float(sums[1]), float(sums[4]), float(maxs[3])
+    else:
+        all_metrics = local_metrics
+        qps, ipm, rows = float(tot[0]), float(tot[1]), float(tot[4])
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    kernel = {"cadmm": "k_cadmm", "dd": "k_dd_setup+k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
+    launch_ms = float(tot[2]) / max(w["hl_steps"], 1)
+    flops_launch = (FLOPS_FIXED * float(tot[1]) + FLOPS_PER_ROW * float(tot[4])) / max(w["hl_steps"], 1)
+    tflops = flops_launch / max(launch_ms * 1e-3, 1e-12) / 1e12
+    work_mode = "fixed work: tol 0, 25 ADMM iterations" if args.fixed_work else "reference loop: tol 1e-2, max_iter 100"
+    workload = f"{cfg}: {args.mode} n={n}, QP-level, no env ({work_mode}), {B} scenarios per GPU"
+    out = {
+        "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
+        "value": qps / elapsed, "unit": "agent-QP solves/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (perturbed rest states, acc_des ~ U(-5,5)^6" + (", randomized payload mass/inertia)" if per_scen else ")"),
+        "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "parallelism": f"scenario-sharded x{world}"},
+        "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
+                  "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
+                  "kernel_ms_per_step": launch_ms},
+        "roofline": {"bound": "fp64-valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kernel, "launch_ms": launch_ms,
+                     "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"
+                                   + (" (C-ADMM lane count, approximate for DD)" if args.mode == "dd" else "")},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline_qp(cfg, n, args.mode, args.cpu_sample_s, args.fixed_work)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
