@@ -914,19 +914,34 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 // rollout / desired acceleration / warm start
 // ------------------------------------------------------------------------------------------------
+// NN > 0: team size known at compile time (every loop over agents unrolls, the state stays in
+// registers); NN = 0: any n <= NMAX from a.n (the state array then lives in scratch).
+template <int NN>
 __global__ __launch_bounds__(64) void k_rollout(KArgs a, int steps, double dt, const double* fdes) {
+  constexpr int NA = NN > 0 ? NN : NMAX;
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
   if (sc >= a.B) return;
-  const int n = a.n;
+  const int n = NN > 0 ? NN : a.n;
+  const int S = DAT_STATE_SIZE(n);
   const double* prm = prm_of(a, sc);
-  double st[DAT_STATE_SIZE(NMAX)];
+  double st[DAT_STATE_SIZE(NA)];
   double* g = a.state + (size_t)sc * a.S;
-  for (int k = 0; k < a.S; ++k) st[k] = g[k];
+  for (int k = 0; k < S; ++k) st[k] = g[k];
   int cnt = a.counter[sc];
   const double* fd = fdes + (size_t)sc * 3 * n;
-  for (int s = 0; s < steps; ++s) sim_step<NMAX>(prm, n, st, &cnt, fd, dt);
-  for (int k = 0; k < a.S; ++k) g[k] = st[k];
+  for (int s = 0; s < steps; ++s) sim_step<NA>(prm, n, st, &cnt, fd, dt);
+  for (int k = 0; k < S; ++k) g[k] = st[k];
   a.counter[sc] = cnt;
+}
+
+void launch_rollout(const KArgs& a, int B, hipStream_t stream, int steps, double dt, const double* fdes) {
+  const dim3 grid((B + 63) / 64), block(64);
+  if (a.n == 3)
+    hipLaunchKernelGGL(k_rollout<3>, grid, block, 0, stream, a, steps, dt, fdes);
+  else if (a.n == 6)
+    hipLaunchKernelGGL(k_rollout<6>, grid, block, 0, stream, a, steps, dt, fdes);
+  else
+    hipLaunchKernelGGL(k_rollout<0>, grid, block, 0, stream, a, steps, dt, fdes);
 }
 
 __global__ void k_desired(KArgs a, double* acc) {
@@ -1422,7 +1437,7 @@ int dat_rollout(dat_handle* h, int steps, const double* f_des) {
   if (f_des) HIPCHK(hipMemcpyAsync(h->fdes, f_des, sizeof(double) * B * 3 * n, hipMemcpyHostToDevice, h->stream));
   if (!h->have_params) return fail("dat_rollout: params not set");
   KArgs a = kargs(h);
-  hipLaunchKernelGGL(k_rollout, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, steps, h->cfg.dt, (const double*)h->fdes);
+  launch_rollout(a, (int)B, h->stream, steps, h->cfg.dt, (const double*)h->fdes);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1436,8 +1451,7 @@ int dat_closed_loop(dat_handle* h, int hl_steps) {
   for (int s = 0; s < hl_steps; ++s) {
     hipLaunchKernelGGL(k_desired, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->acc);
     if (launch_hl(h)) return -1;
-    hipLaunchKernelGGL(k_rollout, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->cfg.hl_every, h->cfg.dt,
-                       (const double*)h->fdes);
+    launch_rollout(a, (int)B, h->stream, h->cfg.hl_every, h->cfg.dt, (const double*)h->fdes);
     HIPCHK(hipGetLastError());
     if (finish_hl(h)) return -1;
   }
