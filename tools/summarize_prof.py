@@ -70,11 +70,19 @@ def main():
     if os.path.exists(tr):
         for r in csv.DictReader(open(tr)):
             dur[kname(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
-    lines += ["", "| kernel | dispatches | mean ms | median ms | min ms | max ms |", "|---|---|---|---|---|---|"]
+    # bench.py launches each per-step kernel once per step: warmup launches, then the timed ones
+    w0, nk = int(os.environ.get("WARMUP", "2")), int(os.environ.get("STEPS", "5"))
+    lines += ["", f"Durations from the kernel-trace pass; `timed mean` = mean over launches {w0}..{w0 + nk - 1} "
+                  f"(the bench's timed steps with --warmup {w0} --steps {nk}; compare with the bench line's "
+                  "roofline.launch_ms).", "",
+              "| kernel | dispatches | mean ms | timed mean ms | median ms | min ms | max ms |",
+              "|---|---|---|---|---|---|---|"]
     for k, v in sorted(dur.items()):
         if k.startswith("__amd_rocclr"):
             continue
-        lines.append(f"| {k} | {len(v)} | {statistics.mean(v):.4f} | {statistics.median(v):.4f} | {min(v):.4f} | {max(v):.4f} |")
+        tv = v[w0:w0 + nk] or v
+        lines.append(f"| {k} | {len(v)} | {statistics.mean(v):.4f} | {statistics.mean(tv):.4f} | "
+                     f"{statistics.median(v):.4f} | {min(v):.4f} | {max(v):.4f} |")
     lines += ["", "| kernel | VGPR | AGPR | SGPR | LDS | scratch |", "|---|---|---|---|---|---|"]
     for k, m in sorted(meta.items()):
         lines.append(f"| {k} | " + " | ".join(m) + " |")
