@@ -19,6 +19,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "../../include/dat.h"
 #include "dat_qp.hpp"
@@ -1330,7 +1331,21 @@ int dat_set_forests(dat_handle* h, int num_forests, const int* tree_offsets, con
   for (int f = 0; f < num_forests; ++f)
     if (tree_offsets[f + 1] < tree_offsets[f]) return fail("dat_set_forests: offsets must be non-decreasing");
   if (dalloc(h, &h->trees, (size_t)(T > 0 ? T : 1) * 3) || dalloc(h, &h->tree_off, num_forests + 1)) return -1;
-  if (T > 0) HIPCHK(hipMemcpyAsync(h->trees, tree_pos, sizeof(double) * 3 * T, hipMemcpyHostToDevice, h->stream));
+  if (T > 0) {
+    // each forest's trees sorted by x: env_rows scans only the x-window of its vision range
+    std::vector<double> sorted((size_t)3 * T);
+    std::vector<int> idx;
+    for (int f = 0; f < num_forests; ++f) {
+      const int b = tree_offsets[f], e = tree_offsets[f + 1];
+      idx.resize(e - b);
+      for (int k = 0; k < e - b; ++k) idx[k] = b + k;
+      std::stable_sort(idx.begin(), idx.end(), [&](int u, int v) { return tree_pos[3 * u] < tree_pos[3 * v]; });
+      for (int k = 0; k < e - b; ++k)
+        for (int c = 0; c < 3; ++c) sorted[(size_t)3 * (b + k) + c] = tree_pos[(size_t)3 * idx[k] + c];
+    }
+    HIPCHK(hipMemcpyAsync(h->trees, sorted.data(), sizeof(double) * 3 * T, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+  }
   HIPCHK(hipMemcpyAsync(h->tree_off, tree_offsets, sizeof(int) * (num_forests + 1), hipMemcpyHostToDevice, h->stream));
   if (scenario_forest) {
     for (int s = 0; s < h->cfg.batch; ++s)

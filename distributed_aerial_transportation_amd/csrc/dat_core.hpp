@@ -408,13 +408,34 @@ DAT_HD double capsule_tree(const double* x0, const double* d, double rc, const d
   } else if (dist2_slope(x0, d, c, 1.0) <= 0.0) {
     t = 1.0;
   } else {
+    // Safeguarded Newton on the monotone slope g(t) = f'(t) inside the bracket [lo, hi] (g(lo) < 0 <
+    // g(hi)): Newton steps where f is smooth, bisection whenever a step leaves the bracket or f''
+    // vanishes.  Converges to the bracket's machine precision in a handful of steps where the
+    // previous plain bisection took ~52.
     double lo = 0.0, hi = 1.0;
-    for (int it = 0; it < 64; ++it) {  // bisection on the monotone slope: t to machine precision
-      double mid = 0.5 * (lo + hi);
-      if (mid <= lo || mid >= hi) break;
-      if (dist2_slope(x0, d, c, mid) < 0.0) lo = mid; else hi = mid;
+    t = 0.5;
+    const double dxy2 = d[0] * d[0] + d[1] * d[1];
+    for (int it = 0; it < 64; ++it) {
+      double px = x0[0] + t * d[0] - c[0], py = x0[1] + t * d[1] - c[1], pz = x0[2] + t * d[2] - c[2];
+      double rho = sqrt(px * px + py * py);
+      double g = 0.0, hs = 0.0;
+      if (rho > DAT_BARK_RADIUS) {
+        double rp = (px * d[0] + py * d[1]) / rho;  // d rho / dt
+        g += 2.0 * (rho - DAT_BARK_RADIUS) * rp;
+        hs += 2.0 * rp * rp + 2.0 * (rho - DAT_BARK_RADIUS) * (dxy2 - rp * rp) / rho;
+      }
+      double az = fabs(pz) - DAT_BARK_HALF_HEIGHT;
+      if (az > 0.0) {
+        g += 2.0 * az * (pz > 0 ? d[2] : -d[2]);
+        hs += 2.0 * d[2] * d[2];
+      }
+      if (g == 0.0) break;
+      if (g < 0.0) lo = t; else hi = t;
+      double tn = (hs > 0.0) ? t - g / hs : 0.5 * (lo + hi);
+      if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
+      if (tn == t || tn <= lo || tn >= hi) break;
+      t = tn;
     }
-    t = 0.5 * (lo + hi);
   }
   double p[3] = {x0[0] + t * d[0], x0[1] + t * d[1], x0[2] + t * d[2]};
   double ds = point_cyl(p, c, p2);
@@ -480,8 +501,17 @@ DAT_HD EnvOut env_rows(const double* prm, int n, const double* st, const double*
   for (int j = 0; j < DAT_NENV; ++j) bd[j] = 1e300;
   int cnt = 0;
   double dmin = 1e300;
-  for (int t = 0; t < ntree; ++t) {
+  // trees are sorted by x (dat_set_forests): only the window |c.x - ctr.x| <= visr + bark radius
+  // can pass the range test below; lower bound by binary search, stop past the upper edge
+  const double reach = visr + DAT_BARK_RADIUS;
+  int t0 = 0;
+  for (int len = ntree; len > 0;) {
+    int half = len >> 1;
+    if (trees[3 * (t0 + half)] < ctr[0] - reach) { t0 += half + 1; len -= half + 1; } else { len = half; }
+  }
+  for (int t = t0; t < ntree; ++t) {
     const double* c = trees + 3 * t;
+    if (c[0] > ctr[0] + reach) break;
     double ex = ctr[0] - c[0], ey = ctr[1] - c[1], ez = ctr[2] - c[2];
     if (sqrt(ex * ex + ey * ey + ez * ez) > visr + DAT_BARK_RADIUS) continue;
     if (agent >= 0) {

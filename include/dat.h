@@ -67,7 +67,7 @@ int dat_device_count(void);
  * (_set_controller_constants, control/rqp_cadmm.py:192-236, rqp_centralized.py:182-225).
  * Resets the warm state to the constructor's (f = f_eq, lambda = 0). */
 int dat_set_params(dat_handle* h, const double* params, int per_scenario);
-/* forests: num_forests layouts; tree_offsets[num_forests+1] index rows of tree_pos (T x 3);
+/* forests: num_forests layouts; tree_offsets[num_forests+1] index rows of tree_pos (T x 3; the handle keeps each forest sorted by x);
  * scenario_forest[B] selects a layout per scenario (NULL: all use layout 0, -1: no env);
  * mountain[num_forests x DAT_MOUNTAIN_SIZE] for the desired-acceleration law.  num_forests = 0
  * removes the environment (env = None in the reference). */

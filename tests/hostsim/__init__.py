@@ -68,7 +68,9 @@ def env_rows(prm, n, st, trees, agent, alpha):
     rhs = np.zeros(10)
     col = ctypes.c_int()
     md = ctypes.c_double()
-    trees = np.ascontiguousarray(trees, dtype=np.float64)
+    trees = np.asarray(trees, dtype=np.float64)
+    # env_rows scans an x-window of x-sorted trees (dat_set_forests sorts each forest the same way)
+    trees = np.ascontiguousarray(trees[np.argsort(trees[:, 0], kind="stable")])
     k = lib().hs_env_rows(p(prm), n, p(st), p(trees), trees.shape[0], agent, ctypes.c_double(alpha),
                           lhs.ctypes.data_as(D), rhs.ctypes.data_as(D), ctypes.byref(col), ctypes.byref(md))
     return lhs[:k], rhs[:k], bool(col.value), md.value
