@@ -88,6 +88,9 @@ struct KArgs {
   int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
   int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
   int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
+  double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
+                                 //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
+  unsigned* emask;               // C-ADMM: [B n] env row mask of the step
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)
@@ -116,7 +119,8 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 //                 they are fixed for the whole ADMM loop, control/rqp_cadmm.py:305), per-scenario
 //                 env class (the largest env-row count among its agents' QPs: 0, <= 2, <= 5,
 //                 <= 10), collision, min env distance, and a sort key (class, previous step's
-//                 ADMM iteration count);
+//                 ADMM iteration count); the rows go to HBM (erows / emask, SoA over agents) and
+//                 k_cadmm loads them when a slot takes the scenario instead of re-running the query;
 //   k_bucket      stable counting sort of the scenario ids by key (one queue per class);
 //   k_cadmm       persistent blocks (CUs x 4) drain the class queues, classes 3, 2, 1, 0 in turn,
 //                 each with its own row-slot instantiation of the IPM (3 + {10, 5, 2, 0} slots:
@@ -178,7 +182,7 @@ __device__ inline int env_class_of(unsigned emask, const double lhs[DAT_NENV][3]
   return c;
 }
 
-__global__ __launch_bounds__(64) void k_env_class(KArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_env_class(KArgs a) {
   __shared__ int nd[64], cl[64];
   __shared__ double md[64];
   const int n = a.n, G = 64 / n, NT = G * n;
@@ -199,6 +203,17 @@ __global__ __launch_bounds__(64) void k_env_class(KArgs a) {
     need = env_class_of(emask, lhs, rhs);
     col = e.collision;
     dist = e.min_env_dist;
+    // hand the rows to k_cadmm (lanes hold consecutive agents: every store is coalesced)
+    const size_t NA = (size_t)a.B * n, g = (size_t)sc * n + i;
+    a.emask[g] = emask;
+#pragma unroll
+    for (int j = 0; j < DAT_NENV; ++j) {
+      if (!((emask >> j) & 1u)) continue;  // only the slots the mask marks are read back
+      a.erows[(4 * j + 0) * NA + g] = lhs[j][0];
+      a.erows[(4 * j + 1) * NA + g] = lhs[j][1];
+      a.erows[(4 * j + 2) * NA + g] = lhs[j][2];
+      a.erows[(4 * j + 3) * NA + g] = rhs[j];
+    }
   }
   nd[lane] = need;
   cl[lane] = col;
@@ -362,12 +377,18 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (fresh) {
       lane_cadmm_static(P, prm, i);
       if (ENV) {
-        const double* trees;
-        int nt;
-        unsigned emask;
-        forest_of(a, sc, &trees, &nt);
+        // the rows k_env_class computed from the same state this step
+        const size_t NA = (size_t)a.B * n, g = (size_t)sc * n + i;
+        const unsigned emask = a.emask[g];
         double lhs[DAT_NENV][3], rhs[DAT_NENV];
-        env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+#pragma unroll
+        for (int j = 0; j < DAT_NENV; ++j) {
+          const bool on = (emask >> j) & 1u;  // unmarked slots are never written (set_env_rows skips them)
+          lhs[j][0] = on ? a.erows[(4 * j + 0) * NA + g] : 0.0;
+          lhs[j][1] = on ? a.erows[(4 * j + 1) * NA + g] : 0.0;
+          lhs[j][2] = on ? a.erows[(4 * j + 2) * NA + g] : 0.0;
+          rhs[j] = on ? a.erows[(4 * j + 3) * NA + g] : 0.0;
+        }
         EnvRows E;
         set_env_rows(P, E, S, emask, lhs, rhs);
         env_to_lds(L.env, lane, E);
@@ -1056,6 +1077,8 @@ struct dat_handle {
   unsigned char* col = nullptr;
   unsigned long long* counters = nullptr;  // DAT_NCOUNTERS: [CNT_STRIDE k + .] of env class k (C-ADMM); [0..2] otherwise
   int *need = nullptr, *slist = nullptr, *scount = nullptr;
+  double* erows = nullptr;     // C-ADMM: env rows of the step, k_env_class -> k_cadmm
+  unsigned* emask = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
   std::vector<void*> allocs;
@@ -1122,6 +1145,8 @@ KArgs kargs(dat_handle* h) {
   a.err = h->err;
   a.counters = h->counters;
   a.need = h->need;
+  a.erows = h->erows;
+  a.emask = h->emask;
   a.slist = h->slist;
   a.scount = h->scount;
   a.qhead = h->scount ? h->scount + 2 * NCLS : nullptr;
@@ -1254,6 +1279,8 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
   if (c.mode == DAT_MODE_CADMM) {
     rc |= dalloc(h, &h->need, B);
+    rc |= dalloc(h, &h->erows, (size_t)B * n * DAT_NENV * 4);
+    rc |= dalloc(h, &h->emask, (size_t)B * n);
     rc |= dalloc(h, &h->slist, B);
     rc |= dalloc(h, &h->scount, 3 * NCLS);
     rc |= dalloc(h, &h->cf, B * n * N3);
