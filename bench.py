@@ -7,6 +7,7 @@ every scenario, fully on device: forest desired-acceleration law + C-ADMM contro
 rows, up to 101 ADMM iterations of n agent QPs each) + 10 simulation steps (SO(3) PD + dynamics).
 
     python bench.py [--gpus N --steps K --warmup W --batch B --n 6 --mode cadmm]
+    python bench.py --config C2|C3|C5 [--fixed-work]   (QP-level configs of SURVEY.md 8(d))
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 The data path has no collective; torch.distributed (RCCL over xGMI when N > 1) is used for the
