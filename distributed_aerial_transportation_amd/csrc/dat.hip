@@ -49,9 +49,16 @@ constexpr double IPM_TOL = 1e-10;
 // scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
 constexpr int NCLS = 4;
 __host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 5 : DAT_NENV; }
-// k_bucket sort key: class x bin of the scenario's previous ADMM iteration count (1, 2, 3, >= 4),
-// so that scenarios sharing a wavefront tend to need the same number of ADMM passes
-constexpr int NIB = 4;
+// k_bucket sort key: class x bin of the scenario's previous ADMM iteration count (1, 2, 3, 4-5,
+// 6-9, 10-17, 18-33, >= 34), so that scenarios sharing a wavefront tend to need the same number of
+// ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
+// tail of the whole launch)
+constexpr int NIB = 8;
+__host__ __device__ inline int iter_bin(int it) {
+  if (it <= 3) return it < 1 ? 0 : it - 1;
+  const int lg = 31 - __builtin_clz((unsigned)(it - 2));  // floor(log2(it - 2)) >= 1
+  return 2 + lg < NIB - 1 ? 2 + lg : NIB - 1;
+}
 constexpr int NKEY = NCLS * NIB;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
 constexpr int DAT_NCOUNTERS = NCLS * CNT_STRIDE;
@@ -227,7 +234,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       c |= cl[ls * n + k];
       m = fmin(m, md[ls * n + k]);
     }
-    const int bin = min(max(a.iters[sc] - 1, 0), NIB - 1);  // previous step's ADMM iterations
+    const int bin = iter_bin(a.iters[sc]);  // previous step's ADMM iterations
     a.need[sc] = cls * NIB + (NIB - 1 - bin);               // longest first within the class
     a.col[sc] = (unsigned char)c;
     a.mind[sc] = m;
