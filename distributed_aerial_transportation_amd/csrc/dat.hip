@@ -663,16 +663,17 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
   }
   __syncthreads();
   // Gauss-Jordan on [H | I] (H is SPD: no pivoting needed)
+  // Each lane owns whole columns of [H | I] (no index division; a row of the tile is contiguous
+  // across lanes, so the LDS accesses are conflict-free); per-element operation order as before.
   for (int k = 0; k < N; ++k) {
     double piv = H[2 * N * k + k];
-    __syncthreads();
-    for (int c = lane; c < 2 * N; c += 64) H[2 * N * k + c] /= piv;
-    __syncthreads();
     for (int r = lane; r < N; r += 64) fac[r] = H[2 * N * r + k];
     __syncthreads();
-    for (int e = lane; e < N * 2 * N; e += 64) {
-      int r = e / (2 * N), c = e % (2 * N);
-      if (r != k) H[2 * N * r + c] -= fac[r] * H[2 * N * k + c];
+    for (int c = lane; c < 2 * N; c += 64) {
+      const double hk = H[2 * N * k + c] / piv;
+      H[2 * N * k + c] = hk;
+      for (int r = 0; r < N; ++r)
+        if (r != k) H[2 * N * r + c] -= fac[r] * hk;
     }
     __syncthreads();
   }
