@@ -632,15 +632,17 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
   __syncthreads();
   // H = A blkdiag(Q_j^-1) A'  (control/rqp_dd.py:642-655); row r of A restricted to block j:
   //   j == agent(r): unit vector e_{3 + comp};  j != agent(r): -e_comp (comp < 3) or -Rt_j[comp-3, :] on f_j
+  // every index below is compile-time after unrolling, so v stays in registers (no scratch)
   auto arow = [&](int r, int j, double* v) {
-    int ag = r / 6, comp = r % 6;
-    for (int k = 0; k < 9; ++k) v[k] = 0.0;
-    if (j == ag) {
-      v[3 + comp] = 1.0;
-    } else if (comp < 3) {
-      v[comp] = -1.0;
-    } else {
-      for (int k = 0; k < 3; ++k) v[k] = -Rts[9 * j + 3 * (comp - 3) + k];
+    const int ag = r / 6, comp = r % 6;
+    const double* rt = Rts + 9 * j + 3 * (comp >= 3 ? comp - 3 : 0);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      double x = 0.0;
+      if (j == ag) x = (k == 3 + comp) ? 1.0 : 0.0;
+      else if (comp < 3) x = (k == comp) ? -1.0 : 0.0;
+      else if (k < 3) x = -rt[k];
+      v[k] = x;
     }
   };
   for (int e = lane; e < N * N; e += 64) {
@@ -651,9 +653,11 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
       arow(r, j, vr);
       arow(c, j, vc);
       const double* Q = Qi + 81 * j;
+#pragma unroll
       for (int p = 0; p < 9; ++p) {
         if (vr[p] == 0.0) continue;
         double t = 0.0;
+#pragma unroll
         for (int q = 0; q < 9; ++q) t += Q[9 * p + q] * vc[q];
         s += vr[p] * t;
       }
