@@ -594,6 +594,13 @@ __device__ void dd_strong_convexity(const double* prm, int n, const double* st, 
   }
 }
 
+// doubles of the [H | I] area of k_dd_setup; it first holds the per-agent [Q_i | I] (162 n), their
+// pivot columns (9 n) and pivot rows (n ints)
+__host__ __device__ inline int dd_setup_hs(int n) {
+  const int N = 6 * n;
+  return 2 * N * N > 171 * n + 1 ? 2 * N * N : 171 * n + 1;
+}
+
 __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N = 6 * n;
@@ -603,31 +610,58 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
   double* Qi = smem;              // n x 81   sym(Q_i^-1)
   double* Rts = Qi + 81 * n;      // n x 9
   double* H = Rts + 9 * n;        // N x 2N   [H | I]
-  double* fac = H + 2 * N * N;    // N
+  double* fac = H + dd_setup_hs(n);  // N
   const double* prm = prm_of(a, sc);
   const double* st = a.state + (size_t)sc * a.S;
+  // Q_i^-1 by Gauss-Jordan with partial pivoting (np.linalg.inv) on [Q_i | I] in LDS, spread over
+  // the wavefront: lane pairs (agent j, column c) update one column each, with the per-element
+  // arithmetic of the serial elimination (pivot column copied before the update).
+  double* Aug = H;                         // n x 9 x 18, in the [H | I] area (built afterwards)
+  double* colk = Aug + 162 * n;            // n x 9: column k before step k's update
+  int* pivr = (int*)(colk + 9 * n);        // n
   if (lane < n) {
-    double Q[81], Aug[9][18];
+    double Q[81];
     dd_strong_convexity(prm, n, st, lane, Q);
     for (int r = 0; r < 9; ++r)
-      for (int c = 0; c < 18; ++c) Aug[r][c] = c < 9 ? Q[9 * r + c] : (c - 9 == r ? 1.0 : 0.0);
-    for (int k = 0; k < 9; ++k) {  // Gauss-Jordan with partial pivoting (np.linalg.inv)
+      for (int c = 0; c < 18; ++c) Aug[162 * lane + 18 * r + c] = c < 9 ? Q[9 * r + c] : (c - 9 == r ? 1.0 : 0.0);
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * lane, st + DAT_S_RL(n), Rts + 9 * lane);
+  }
+  __syncthreads();
+  for (int k = 0; k < 9; ++k) {
+    if (lane < n) {
+      const double* A = Aug + 162 * lane;
       int p = k;
       for (int r = k + 1; r < 9; ++r)
-        if (fabs(Aug[r][k]) > fabs(Aug[p][k])) p = r;
-      if (p != k)
-        for (int c = 0; c < 18; ++c) { double t = Aug[k][c]; Aug[k][c] = Aug[p][c]; Aug[p][c] = t; }
-      double inv = 1.0 / Aug[k][k];
-      for (int c = 0; c < 18; ++c) Aug[k][c] *= inv;
-      for (int r = 0; r < 9; ++r) {
-        if (r == k) continue;
-        double f = Aug[r][k];
-        for (int c = 0; c < 18; ++c) Aug[r][c] -= f * Aug[k][c];
-      }
+        if (fabs(A[18 * r + k]) > fabs(A[18 * p + k])) p = r;
+      pivr[lane] = p;
     }
-    for (int r = 0; r < 9; ++r)
-      for (int c = 0; c < 9; ++c) Qi[81 * lane + 9 * r + c] = 0.5 * (Aug[r][9 + c] + Aug[c][9 + r]);
-    make_Rt(prm + DAT_P_RCOM(n) + 3 * lane, st + DAT_S_RL(n), Rts + 9 * lane);
+    __syncthreads();
+    for (int e = lane; e < 18 * n; e += 64) {  // row exchange k <-> p, column by column
+      const int j = e / 18, c = e - 18 * j, p = pivr[j];
+      double* A = Aug + 162 * j;
+      if (p != k) { double t = A[18 * k + c]; A[18 * k + c] = A[18 * p + c]; A[18 * p + c] = t; }
+    }
+    __syncthreads();
+    for (int e = lane; e < 9 * n; e += 64) {
+      const int j = e / 9, r = e - 9 * j;
+      colk[e] = Aug[162 * j + 18 * r + k];
+    }
+    __syncthreads();
+    for (int e = lane; e < 18 * n; e += 64) {
+      const int j = e / 18, c = e - 18 * j;
+      double* A = Aug + 162 * j;
+      const double inv = 1.0 / colk[9 * j + k];
+      const double hk = A[18 * k + c] * inv;
+      A[18 * k + c] = hk;
+      for (int r = 0; r < 9; ++r)
+        if (r != k) A[18 * r + c] -= colk[9 * j + r] * hk;
+    }
+    __syncthreads();
+  }
+  for (int e = lane; e < 81 * n; e += 64) {
+    const int j = e / 81, rc = e - 81 * j, r = rc / 9, c = rc - 9 * r;
+    const double* A = Aug + 162 * j;
+    Qi[e] = 0.5 * (A[18 * r + 9 + c] + A[18 * c + 9 + r]);
   }
   __syncthreads();
   // H = A blkdiag(Q_j^-1) A'  (control/rqp_dd.py:642-655); row r of A restricted to block j:
@@ -1172,7 +1206,7 @@ size_t dd_lds(int n) {
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
-  return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + 2 * (size_t)N * N + N);
+  return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + dd_setup_hs(n) + N);
 }
 
 int launch_hl(dat_handle* h) {
