@@ -69,6 +69,8 @@ def parse():
                     help="C2/C5 mode (ii): tol 0, 25 ADMM iterations (test/control/test_rqpcontrollers.py:106-110)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU-only check of the launch / shard / combine path (gloo, no solver work, synthetic numbers)")
     args = ap.parse_args()
     n, mode, batch = QP_CONFIGS.get(args.config, (6, "cadmm", 65536))
     args.n = n if args.n is None else args.n
@@ -179,51 +181,137 @@ def combine_ranks(dist, world: int, tot: np.ndarray, metrics: np.ndarray, device
     return t.cpu().numpy(), mx.cpu().numpy(), torch.cat(gath).cpu().numpy()
 
 
+def spawn_ranks(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes (one per GPU) with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, exactly as torch.distributed.run would, and exit
+    with the worst rank's code.  This parent process never touches the GPU (no HIP call, no
+    torch.cuda), so the ranks own their devices; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+class _SelftestEngine:
+    """--selftest: stands in for BatchedController so the launch / sharding / rank-combination path of
+    this script can be exercised on a CPU-only host (gloo).  It performs no solver work and its
+    numbers are synthetic; the JSON line says so ("data": "selftest")."""
+
+    def __init__(self, n: int, batch: int, rank: int) -> None:
+        self.n, self.batch, self.rank, self.steps = n, batch, rank, 0
+
+    def set_forests(self, *a, **k):
+        pass
+
+    def set_state(self, *a, **k):
+        pass
+
+    def closed_loop(self, k):
+        self.steps += k
+
+    def reset_counters(self):
+        self.steps = 0
+
+    def synchronize(self):
+        pass
+
+    def work(self):
+        q = self.steps * self.batch * self.n
+        return {"qp_solves": q, "ipm_iters": 7 * q, "ipm_row_iters": 35 * q, "hl_steps": self.steps,
+                "hl_kernel_ms": 1.0 * self.steps}
+
+    def class_work(self, k):
+        w = self.work()
+        return dict(w, kernel_ms=w["hl_kernel_ms"], slot_ipm_iters=w["ipm_iters"], wave_admm_iters=w["qp_solves"] // self.n)
+
+    def control(self, *a):
+        from types import SimpleNamespace
+
+        return SimpleNamespace(iters=np.full(self.batch, 1 + self.rank, dtype=np.int32),
+                               min_env_dist=np.full(self.batch, 1.0), collision=np.zeros(self.batch, dtype=bool))
+
+
+def timed_steps(eng, steps: int, barrier):
+    """Run `steps` closed-loop HL periods one at a time (each synchronised), bracketed by the
+    barrier + device synchronisation; returns (elapsed s, per-step ms array)."""
+    barrier()
+    eng.synchronize()
+    per = np.empty(steps)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ts = time.perf_counter()
+        eng.closed_loop(1)
+        eng.synchronize()
+        per[k] = (time.perf_counter() - ts) * 1e3
+    t1 = time.perf_counter()
+    barrier()
+    return t1 - t0, per
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
-    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+        if args.selftest:
+            dist.init_process_group("gloo", init_method="env://")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", init_method="env://")
+    dev = "cpu" if args.selftest else f"cuda:{local}"
 
     if args.config != "C4":
+        if args.selftest:
+            sys.exit("bench.py: --selftest covers the C4 path only")
         return qp_level(args, dist, rank, world, local)
     n, B = args.n, args.batch
     scen_forest, seed = shard(rank, B, args.forests)
     rng = np.random.default_rng(seed)
-    forests = [Forest.seeded(s) for s in range(args.forests)]
-    if args.start == "path":
-        states = scenarios.forest_path_states(n, B, rng, forests, scen_forest)
+    if args.selftest:
+        eng = _SelftestEngine(n, B, rank)
     else:
-        states = scenarios.forest_start_states(n, B, rng)
-    eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
-    eng.set_forests(forests, scen_forest)
-    eng.set_state(states, np.zeros(B, dtype=np.int32))
+        from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+
+        forests = [Forest.seeded(s) for s in range(args.forests)]
+        if args.start == "path":
+            states = scenarios.forest_path_states(n, B, rng, forests, scen_forest)
+        else:
+            states = scenarios.forest_start_states(n, B, rng)
+        eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
+        eng.set_forests(forests, scen_forest)
+        eng.set_state(states, np.zeros(B, dtype=np.int32))
     eng.closed_loop(args.warmup)
     eng.reset_counters()
 
     def barrier():
         if dist is not None:
-            import torch
+            if not args.selftest:
+                import torch
 
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
             dist.barrier()
 
-    barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    eng.closed_loop(args.steps)
-    eng.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
+    elapsed, per_step = timed_steps(eng, args.steps, barrier)
     work = eng.work()
     qps, ipm, hl_steps, hl_ms = work["qp_solves"], work["ipm_iters"], work["hl_steps"], work["hl_kernel_ms"]
     row_it = work["ipm_row_iters"]
@@ -232,7 +320,7 @@ def main():
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
     tot = np.array([qps, ipm, hl_ms, elapsed, row_it], dtype=np.float64)
     if dist is not None:
-        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, f"cuda:{local}")
+        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, dev)
         qps_all, ipm_all, row_all = float(sums[0]), float(sums[1]), float(sums[4])
         elapsed = float(maxs[3])
         hl_ms_rank0 = float(tot[2])
@@ -274,11 +362,14 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        "ms_per_step_p50": float(np.percentile(per_step, 50)),
+        "ms_per_step_p99": float(np.percentile(per_step, 99)),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"synthetic (seeded forests 0..63, randomized C4 {args.start} start states)",
+        "data": ("selftest (no solver work; synthetic counters)" if args.selftest else
+                 f"synthetic (seeded forests 0..63, randomized C4 {args.start} start states)"),
         "config": {"workload": workload,
                    "n": n, "scenarios_per_gpu": B, "hl_every": 10, "dt": 1e-3, "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
@@ -291,7 +382,7 @@ def main():
                      "flops_per_launch": flops_launch,
                      "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"},
     }
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and not args.selftest:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start)
     print(json.dumps(out), flush=True)
     if dist is not None:
@@ -334,10 +425,13 @@ def qp_level(args, dist, rank: int, world: int, local: int):
 
     barrier()
     eng.synchronize()
+    per_step = np.empty(args.steps)
     t0 = time.perf_counter()
     for k in range(args.steps):
+        ts = time.perf_counter()
         step(args.warmup + k)
-    eng.synchronize()
+        eng.synchronize()
+        per_step[k] = (time.perf_counter() - ts) * 1e3
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -364,7 +458,9 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
         "value": qps / elapsed, "unit": "agent-QP solves/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step_p50": float(np.percentile(per_step, 50)), "ms_per_step_p99": float(np.percentile(per_step, 99)),
+        "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (perturbed rest states, acc_des ~ U(-5,5)^6" + (", randomized payload mass/inertia)" if per_scen else ")"),
         "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "parallelism": f"scenario-sharded x{world}"},

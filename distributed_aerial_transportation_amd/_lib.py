@@ -88,6 +88,7 @@ EXPORTS = {
     "dat_get_class_occupancy": (ctypes.c_int, [H, ctypes.c_int, LL, LL]),
     "dat_reset_counters": (ctypes.c_int, [H]),
     "dat_synchronize": (ctypes.c_int, [H]),
+    "dat_set_persistent_blocks": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_env_rows": (ctypes.c_int, [H, D, D, I, U8, D]),
 }
 

@@ -123,6 +123,10 @@ class BatchedController:
         L.check(self._lib.dat_set_max_iter(self._h, int(max_iter)))
         self.cfg.max_iter = max_iter
 
+    def set_persistent_blocks(self, blocks: int) -> None:
+        """C-ADMM: resident k_cadmm workgroups draining the scenario queues (0: default)."""
+        L.check(self._lib.dat_set_persistent_blocks(self._h, int(blocks)))
+
     def reset_warm_start(self) -> None:
         L.check(self._lib.dat_reset_warm_start(self._h))
 

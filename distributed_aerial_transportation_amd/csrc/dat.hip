@@ -762,6 +762,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
     }
     for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
+    for (int c = 0; c < 9; ++c) myX[c] = prev[c];  // the controller's current (f, F, M)
     if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
   }
   if (lane < 64) red[lane * DD_RS + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
@@ -815,10 +816,13 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int c = 0; c < 3; ++c) prev[c] = y[0][c];
         for (int c = 0; c < 6; ++c) prev[3 + c] = w[c];
       } else if (o.status == ST_FAILED) {  // control/rqp_dd.py:484-489
+        // Quirk a15: the controller's f aliases solver 0's f_eq (control/rqp_dd.py:629, written in
+        // place at :725), so agent 0's fallback sums the controller's current forces (every agent's
+        // f before this iteration's writes); the other agents sum their own f_eq.
         const double* feq = prm + DAT_P_FEQ(n);
         double s3[3] = {0, 0, 0}, jr[3], rf[3];
         for (int k = 0; k < n; ++k)
-          for (int c = 0; c < 3; ++c) s3[c] += feq[3 * k + c];
+          for (int c = 0; c < 3; ++c) s3[c] += (i == 0) ? X[(ls * n + k) * 9 + c] : feq[3 * k + c];
         for (int c = 0; c < 3; ++c) { prev[c] = feq[3 * i + c]; prev[3 + c] = s3[c] - feq[3 * i + c]; }
         cross3(prm + DAT_P_RCOM(n) + 3 * i, prev, rf);
         mv3(prm + DAT_P_JTI, rf, jr);
@@ -1603,6 +1607,19 @@ int dat_reset_counters(dat_handle* h) {
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
   h->hl_ms = 0.0;
+  return 0;
+}
+
+int dat_set_persistent_blocks(dat_handle* h, int blocks) {
+  if (!h) return fail("null handle");
+  if (blocks < 0) return fail("dat_set_persistent_blocks: negative");
+  if (blocks == 0) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->cfg.device) != hipSuccess || ncu <= 0)
+      ncu = 256;
+    blocks = 4 * ncu;
+  }
+  h->persistent_blocks = blocks;
   return 0;
 }
 

@@ -635,6 +635,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     double dv[3], dw[3];
     double rk[NB][3], Rf[6];
     double dres = 0.0, pres = 0.0, gap = 0.0;
+    double chk = 0.0;  // plain sum of every residual entry: NaN / Inf propagate (fmax drops NaN)
     {
       double u[6], pi[6], az[6];
       compute_u(u);
@@ -652,6 +653,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         for (int c = 0; c < 3; ++c) {
           rk[k][c] = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
           dres = fmax(dres, fabs(rk[k][c]));
+          chk += rk[k][c];
         }
       }
       if (MODE == MODE_CADMM) {
@@ -667,7 +669,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         for (int r = 0; r < 6; ++r) Rf[r] = 0.0;
       }
 #pragma unroll
-      for (int r = 0; r < 6; ++r) dres = fmax(dres, fabs(Rf[r]));
+      for (int r = 0; r < 6; ++r) {
+        dres = fmax(dres, fabs(Rf[r]));
+        chk += Rf[r];
+      }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         double rz[9];
@@ -675,16 +680,19 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
           pres = fmax(pres, fabs(rz[j]));
+          chk += rz[j];
           gap += sk[k][j] * zk[k][j];
         }
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        pres = fmax(pres, fabs(sl[l] - (rowdot(l, dv, dw) + rb(l))));
+        const double rl = sl[l] - (rowdot(l, dv, dw) + rb(l));
+        pres = fmax(pres, fabs(rl));
+        chk += rl;
         gap += sl[l] * zl[l];
       }
       out.iters = it;
-      if (!(dres == dres) || !(pres == pres) || !(gap == gap)) {  // NaN
+      if (!(fabs(chk + gap) < 1e300)) {  // NaN or Inf anywhere in the residuals
         out.status = ST_FAILED;
         break;
       }

@@ -233,8 +233,13 @@ class DD:
         r = solve_qp(P, q, G, h, dims, A, b)
         self.qp_iters.append(r.iters)
         if r.status == NUMERICAL:
+            # exception -> equilibrium forces (control/rqp_dd.py:484-489).  Quirk a15: the
+            # controller's f IS solver 0's f_eq (control/rqp_dd.py:629, written in place at :725), so
+            # agent 0's fallback F_0 = sum of the controller's current f - fi_eq (fi_eq itself is a
+            # separate array, :173,181); the other agents read their own, unaliased f_eq.
             fi = self.f_eq[:, i].copy()
-            self.prev[i] = (fi, np.sum(self.f_eq, axis=1) - fi, -self.p.JT_inv @ skew(self.p.r_com[:, i]) @ fi)
+            fsum = np.sum(self.f, axis=1) if i == 0 else np.sum(self.f_eq, axis=1)
+            self.prev[i] = (fi, fsum - fi, -self.p.JT_inv @ skew(self.p.r_com[:, i]) @ fi)
         elif r.status == OPTIMAL:
             self.prev[i] = (r.x[9:12].copy(), r.x[12:15].copy(), r.x[15:18].copy())
         return self.prev[i], r

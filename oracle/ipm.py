@@ -36,6 +36,7 @@ import numpy as np
 OPTIMAL = 0
 MAX_ITER = 1
 NUMERICAL = 2
+INFEASIBLE = 3  # a linear row 0'x <= h_j with h_j < 0: primal infeasible (Clarabel reports "infeasible")
 
 
 @dataclass
@@ -180,6 +181,14 @@ def solve_qp(P, q, G, h, dims: ConeDims, A=None, b=None, tol=1e-11, max_iter=80)
         b = np.zeros(0)
     p = A.shape[0]
     e = _e(dims)
+    z0 = np.zeros(n)
+    if not all(np.all(np.isfinite(v)) for v in (P, q, G, h, A, b)):
+        # non-finite problem data: the solver errors out (the reference's exception branch)
+        return IPMResult(z0, np.zeros(m), np.zeros(m), np.zeros(p), NUMERICAL, 0, np.nan, np.nan, np.nan, np.nan)
+    zero_rows = ~np.any(G[: dims.l] != 0.0, axis=1)
+    if np.any(zero_rows & (h[: dims.l] < 0.0)):
+        # 0 <= h_j < 0 cannot hold: certificate of primal infeasibility without iterating
+        return IPMResult(z0, np.zeros(m), np.zeros(m), np.zeros(p), INFEASIBLE, 0, np.inf, np.nan, np.nan, np.nan)
 
     # Initial point: least-squares KKT with W = I, then shift into the cone interior.
     K0 = np.zeros((n + p + m, n + p + m))

@@ -57,3 +57,24 @@ def test_combine_ranks_gloo_world2(tmp_path):
     # all-gather keeps rank order, each rank's shard of scenarios contiguous
     assert np.array_equal(g[:B, 0], np.zeros(B)) and np.array_equal(g[B:, 0], np.ones(B))
     assert np.array_equal(g[:, 1], np.arange(world * B) % 64)
+
+
+def test_bench_spawns_ranks_selftest():
+    """`python bench.py --gpus 2` without a launcher spawns two rank processes (gloo here, --selftest:
+    no solver work) that shard, combine over the process group and print ONE line from rank 0."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--selftest", "--steps", "2",
+                        "--warmup", "1", "--batch", "16"], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "scenario-sharded x2"
+    assert out["stats"]["agent_qp_solves"] == 2 * 2 * 16 * 6  # ranks x steps x scenarios x agents
+    assert out["stats"]["mean_admm_iters"] == 1.5             # gathered from both ranks (1 and 2)
+    assert out["data"].startswith("selftest")

@@ -1,0 +1,176 @@
+"""GPU parity on the headline workload (config C4): 6-quadrotor C-ADMM in the forest through the
+production path k_env_class -> erows -> k_cadmm (persistent drain with slot refill).
+
+Reference: control/rqp_cadmm.py:307-373 (env CBF rows feeding each agent QP), :631-675 (the ADMM
+loop, whose per-scenario semantics must not depend on which workgroup slot runs the scenario),
+example/rqp_example.py:33-59,120-131 (desired acceleration law, HL step + 10 simulation steps).
+
+Scenarios start 0.25-1.5 m (capsule surface to bark) in front of a tree and head towards it, so
+env rows bind in many agent QPs.  The k_cadmm grid is capped at two workgroups (20 scenario slots
+for 120 scenarios), so every slot is refilled several times within each control step and the
+per-class queues are claimed by more than one workgroup.  Two HL periods are run (control, 10
+simulation steps, control): the second step runs from the warm state (f, f_mean, lambda) the
+first one left.  Every scenario is checked for OPTIMAL agent QPs and a sane iteration count; a
+sample is checked against the oracle: iteration counts exact, f_des within 1e-5 relative,
+residual sequences within 1e-4 relative, states after the rollout within 1e-9.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import controllers as oc
+from oracle import forest as of
+from oracle import model as om
+from oracle import scenarios as osc
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+N = 6
+TOL = 1e-2
+
+
+def _oforest(f):
+    o = of.Forest.__new__(of.Forest)
+    o.tree_pos = f.tree_pos.copy()
+    o.num_trees = f.tree_pos.shape[0]
+    o.mountain_center, o.mountain_radius = f.mountain_center, f.mountain_radius
+    o.bark_radius = f.bark_radius
+    o.mountain_sphere_radius, o.mountain_center_depth = f.mountain_sphere_radius, f.mountain_center_depth
+    return o
+
+
+def near_tree_states(n, forests, scen_forest, rng, d_axis=(1.6, 2.8), speed=(0.5, 1.0)):
+    """Payload 1.6-2.8 m (xy) from a tree axis, moving towards it (heading within +-0.3 rad), at
+    terrain height + 1.5, rest attitude; positions closer than 1.5 m to any tree axis are redrawn."""
+    from distributed_aerial_transportation_amd import scenarios, system
+
+    tmpl = system.pack_state(scenarios.rest_state(n))
+    out = np.tile(tmpl, (len(scen_forest), 1))
+    for b, f in enumerate(scen_forest):
+        F = forests[f]
+        inner = np.nonzero((F.tree_pos[:, 0] > 8.0) & (F.tree_pos[:, 0] < 50.0))[0]
+        while True:
+            k = rng.choice(inner)
+            th = rng.uniform(-0.3, 0.3)
+            head = np.array([np.cos(th), np.sin(th)])
+            xy = F.tree_pos[k, :2] - rng.uniform(*d_axis) * head
+            if np.min(np.linalg.norm(F.tree_pos[:, :2] - xy, axis=1)) >= 1.5:
+                break
+        sp = rng.uniform(*speed)
+        out[b, 12 * n:12 * n + 3] = [xy[0], xy[1], F.terrain_height(xy) + 1.5]
+        out[b, 12 * n + 3:12 * n + 6] = [sp * head[0], sp * head[1], 0.0]
+    return out
+
+
+def _ostate(x, n):
+    from distributed_aerial_transportation_amd.system import RQPState
+
+    s = RQPState.unpack(x, n)
+    return om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
+
+
+class _EnvProbe(oc.CADMM):
+    """Oracle C-ADMM that records the largest env-row multiplier of every agent solve."""
+
+    zmax = 0.0
+
+    def solve_agent(self, i, s, acc_des, env, rho):
+        P, q, G, h, dims, A, b = om.build_qp("cadmm", self.p, self.c, s, acc_des, env, i=i, f_eq=self.f_eq,
+                                             lam=self.lam[:, :, i], rho=rho, f_mean=self.f_mean)
+        out = super().solve_agent(i, s, acc_des, env, rho)
+        # linear rows: f_z, 3 base CBF rows, then the (nonzero) env rows (oracle/model.py:364-378)
+        r = out[1]
+        if dims.l > 4:
+            self.zmax = max(self.zmax, float(np.max(r.z[4:dims.l])))
+        return out
+
+
+def _ambiguous(err_seq, it, tol=TOL):
+    """The reference stops when res < tol; a residual within 1e-7 relative of tol can flip the count."""
+    seq = list(err_seq)
+    return any(abs(e - tol) < 1e-7 * tol for e in seq)
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+@pytest.fixture(scope="module")
+def c4_run():
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+
+    B = 120  # 64 // 6 = 10 scenarios per wavefront: 12 wavefronts' worth through 2 resident workgroups
+    forests = [Forest.seeded(s) for s in range(4)]
+    sf = np.arange(B) % 4
+    rng = np.random.default_rng(2024)
+    x0 = near_tree_states(N, forests, sf, rng)
+    eng = BatchedController("cadmm", N, B, scenarios.params_block(N), record_err=True)
+    eng.set_forests(forests, sf)
+    eng.set_persistent_blocks(2)
+    eng.set_state(x0, np.zeros(B, dtype=np.int32))
+    r1 = eng.control(None, None)  # forest desired-acceleration law on the device
+    eng.rollout(10)
+    x1, cnt = eng.get_state()
+    r2 = eng.control(None, None)
+    w = eng.work()
+    cls = [eng.class_work(k) for k in range(4)]
+    return dict(forests=forests, sf=sf, x0=x0, x1=x1, cnt=cnt, r1=r1, r2=r2, work=w, classes=cls, B=B)
+
+
+def test_c4_all_scenarios_sane(c4_run):
+    """Every agent QP of both steps solved to OPTIMAL, ADMM counts in [1, max_iter + 1], forces
+    finite, and the env classes 1-3 (binding-capable rows) actually ran."""
+    for r in (c4_run["r1"], c4_run["r2"]):
+        assert np.all(r.qp_status == 0), np.argwhere(r.qp_status != 0)
+        assert np.all((r.iters >= 1) & (r.iters <= 101))
+        assert np.all(np.isfinite(r.f_des))
+        assert not np.any(r.collision)
+    env_qps = sum(c["qp_solves"] for c in c4_run["classes"][1:])
+    assert env_qps > 0.5 * c4_run["work"]["qp_solves"], c4_run["classes"]
+    # slot refill: more scenarios than the 2 x 10 resident slots, all completed
+    assert c4_run["work"]["qp_solves"] >= 2 * c4_run["B"] * N
+
+
+def test_c4_sample_matches_oracle(c4_run):
+    from distributed_aerial_transportation_amd import system  # noqa: F401
+
+    B, r1, r2 = c4_run["B"], c4_run["r1"], c4_run["r2"]
+    # the scenarios nearest to a tree (most env rows) plus a few others
+    order = np.argsort(r1.min_env_dist)
+    sample = list(order[:10]) + list(np.random.default_rng(1).choice(order[10:], 4, replace=False))
+    p = osc.params(N)
+    checked, ambiguous, binding = 0, 0, 0
+    for b in sample:
+        of_ = _oforest(c4_run["forests"][c4_run["sf"][b]])
+        ctl = _EnvProbe(p, osc.col_radius(N), of_)
+        s = _ostate(c4_run["x0"][b], N)
+        acc, _, _ = oc.desired_acceleration_forest(s, of_)
+        f1, st1 = ctl.control(s, acc)
+        for _ in range(10):
+            f, M = om.low_level_control(p, s, f1)
+            s.integrate(*om.forward_dynamics(p, s, f, M), 1e-3)
+        np.testing.assert_allclose(c4_run["x1"][b], _xflat(s, N), atol=1e-9, rtol=0)
+        acc2, _, _ = oc.desired_acceleration_forest(s, of_)
+        f2, st2 = ctl.control(s, acc2)
+        if _ambiguous(st1.err_seq, st1.iter) or _ambiguous(st2.err_seq, st2.iter):
+            ambiguous += 1
+            continue
+        assert r1.iters[b] == st1.iter, (b, r1.iters[b], st1.iter)
+        assert _rel(r1.f_des[b], f1) < REL, (b, _rel(r1.f_des[b], f1))
+        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=1e-4, atol=1e-7)
+        assert r2.iters[b] == st2.iter, (b, r2.iters[b], st2.iter)
+        assert _rel(r2.f_des[b], f2) < REL, (b, _rel(r2.f_des[b], f2))
+        np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=1e-4, atol=1e-7)
+        assert bool(r1.collision[b]) == bool(st1.collision)
+        assert r1.min_env_dist[b] == pytest.approx(st1.min_env_dist, abs=1e-8)
+        checked += 1
+        binding += ctl.zmax > 1e-6
+    assert ambiguous <= 1 and checked >= len(sample) - 1
+    assert binding >= 3, f"only {binding} sampled scenarios had a binding env row"
+
+
+def _xflat(s, n):
+    from distributed_aerial_transportation_amd import system
+
+    return system.pack_state(s)
