@@ -17,6 +17,13 @@ from tests._golden import load, state_from, unpack_flat
 pytestmark = pytest.mark.gpu
 
 REL = 1e-5
+# Residual sequences (err_seq) are consensus errors F_i - sum_j f_j: differences of forces of order
+# m_T g (17-30 N) that shrink to ~1e-2, so they inherit the agent-QP solution error amplified by that
+# cancellation.  tools/dd_sensitivity.py runs the ORACLE against itself on the DD step test's
+# scenarios: IPM tolerance 1e-10 vs 1e-11 moves err_seq by up to 9.6e-5 relative (1.3e-6 N
+# absolute at err ~ 1e-2), 1e-12 vs 1e-11 by 1.6e-5, while an explicit H^-1 instead of cho_solve
+# moves it by 2e-11.  The comparison is therefore rtol 1e-4 OR 2e-6 N absolute (1e-7 of m_T g).
+ERR_RTOL, ERR_ATOL = 1e-4, 2e-6
 
 
 def _eng(mode, n, B, **kw):
@@ -149,8 +156,8 @@ def test_gpu_dd_step_matches_oracle(n):
             continue
         assert r1.iters[b] == st1.iter and r2.iters[b] == st2.iter, (b, r1.iters[b], st1.iter, r2.iters[b], st2.iter)
         assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL, (_rel(r1.f_des[b], f1), _rel(r2.f_des[b], f2))
-        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=1e-4, atol=1e-9)
-        np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=1e-4, atol=1e-9)
+        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
+        np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
         assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
     assert skipped <= 1
 
@@ -210,7 +217,7 @@ def test_gpu_dd_golden():
         assert r.iters[0] == d["tol_iters"][k]
         assert _rel(r.f_des[0], d["tol_f"][k]) < REL
         it = int(d["tol_iters"][k])
-        np.testing.assert_allclose(r.err_seq[0, : it - 1], d["tol_err"][k][: it - 1], rtol=1e-4, atol=1e-9)
+        np.testing.assert_allclose(r.err_seq[0, : it - 1], d["tol_err"][k][: it - 1], rtol=ERR_RTOL, atol=ERR_ATOL)
 
 
 def test_gpu_centralized_golden():
@@ -312,7 +319,7 @@ def test_gpu_failure_branches(mode):
         assert _rel(r1.f_des[b], f1) < REL, (b, r1.f_des[b], f1)
         assert r1.iters[b] == st1.iter, (b, r1.iters[b], st1.iter)
         if mode != "centralized":  # DD scenario 2: err_seq[0] carries quirk a15's sum of current forces
-            np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=1e-4, atol=1e-9)
+            np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
     # infeasible: the previous step's forces are held
     assert _rel(r1.f_des[1], r0.f_des[1]) < 1e-12
     if mode == "cadmm":

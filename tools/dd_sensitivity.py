@@ -1,0 +1,73 @@
+"""How sensitive are DD residual sequences to the agent-QP solve accuracy?  (CPU, oracle only)
+
+Runs the oracle DD controller (oracle/controllers.py::DD, control/rqp_dd.py:695-752) on the
+scenarios of tests/test_gpu_parity.py::test_gpu_dd_step_matches_oracle[6] (two consecutive steps,
+warm multipliers) and compares its err_seq against itself with
+  * the IPM stopping tolerance changed (1e-11 is the oracle default, 1e-10 the device IPM's);
+  * cho_factor / cho_solve (control/rqp_dd.py:657,688) replaced by an explicit H^-1.
+Measured (round 2): tol 1e-10 -> 9.6e-5 max relative change, 1e-9 -> 3.4e-3, 1e-12 -> 1.6e-5,
+explicit inverse -> 2.0e-11.  The DD err_seq drift between the GPU and the oracle is therefore the
+QP solve tolerance amplified by the consensus-error cancellation, not the H solve.
+
+    python tools/dd_sensitivity.py
+"""
+
+import os
+import sys
+
+import numpy as np
+import scipy.linalg as sl
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import oracle.controllers as oc  # noqa: E402
+import oracle.ipm as oi  # noqa: E402
+from oracle import model as om, scenarios as osc  # noqa: E402
+from distributed_aerial_transportation_amd import scenarios  # noqa: E402
+from distributed_aerial_transportation_amd.system import RQPState  # noqa: E402
+
+
+def main():
+    n, B = 6, 6
+    rng = np.random.default_rng(10 + n)
+    states = scenarios.perturbed_states(n, B, rng)
+    acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
+
+    def ost(x):
+        s = RQPState.unpack(x, n)
+        return om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
+
+    orig = oi.solve_qp
+
+    def run(tol, inv=False):
+        oc.solve_qp = lambda *a, **k: orig(*a, **{**k, "tol": tol})
+        if inv:
+            oc.cho_factor = lambda H: np.linalg.inv(H)
+            oc.cho_solve = lambda Hi, b: Hi @ b
+        out = []
+        for b in range(B):
+            ctl = oc.DD(osc.params(n), osc.col_radius(n))
+            s = ost(states[b])
+            _, st1 = ctl.control(s, (acc[b, :3], acc[b, 3:]))
+            _, st2 = ctl.control(s, (acc[B - 1 - b, :3], acc[B - 1 - b, 3:]))
+            out.append((np.array(st1.err_seq), np.array(st2.err_seq)))
+        oc.solve_qp, oc.cho_factor, oc.cho_solve = orig, sl.cho_factor, sl.cho_solve
+        return out
+
+    base = run(1e-11)
+    for tol, inv in [(1e-10, False), (1e-9, False), (1e-12, False), (1e-11, True)]:
+        o = run(tol, inv)
+        m = 0.0
+        for (a1, a2), (b1, b2) in zip(base, o):
+            if a1.shape != b1.shape or a2.shape != b2.shape:
+                m = np.inf
+                break
+            for x, y in ((a1, b1), (a2, b2)):
+                if x.size:
+                    m = max(m, float(np.max(np.abs(x / y - 1.0))))
+        print(f"ipm tol {tol:g}  explicit H^-1 {inv}:  max relative err_seq change {m:.3g}")
+
+
+if __name__ == "__main__":
+    main()
