@@ -7,6 +7,7 @@ the controllers raise.  ``build()`` compiles the library in-tree for gfx950 with
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -46,14 +47,33 @@ class Config(ctypes.Structure):
     ]
 
 
+def source_hash() -> str:
+    """sha256 of the library's sources (the build stamp next to libdat.so records the one it was built from)."""
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+STAMP = LIB_PATH + ".srchash"
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile libdat.so (gfx950) next to this file if it is missing or stale."""
-    stale = not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(os.path.getmtime(d) for d in DEPS)
-    if force or stale:
+    """Compile libdat.so (gfx950) next to this file unless it exists and was built from the current
+    sources (content hash, not file times: a copied tree keeps its stamp)."""
+    want = source_hash()
+    have = None
+    if os.path.exists(LIB_PATH) and os.path.exists(STAMP):
+        with open(STAMP) as f:
+            have = f.read().strip()
+    if force or have != want:
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", SRC, "-o", LIB_PATH]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise DatError("hipcc failed:\n" + r.stderr[-4000:])
+        with open(STAMP, "w") as f:
+            f.write(want + "\n")
         if verbose:
             print(" ".join(cmd))
     return LIB_PATH
@@ -90,6 +110,7 @@ EXPORTS = {
     "dat_synchronize": (ctypes.c_int, [H]),
     "dat_set_persistent_blocks": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_env_rows": (ctypes.c_int, [H, D, D, I, U8, D]),
+    "dat_solve_agent_qp_batch": (ctypes.c_int, [H, ctypes.c_int, I, I, D, D, D, D, D, D, I, I, U8, D]),
 }
 
 

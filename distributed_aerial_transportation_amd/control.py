@@ -27,7 +27,8 @@ import numpy as np
 
 from . import _lib as L
 from . import layout
-from .system import RQPCollision, RQPParameters, RQPState, pack_mountain, pack_params, pack_state
+from .system import (RQPCollision, RQPParameters, RQPState, _skew, equilibrium_forces, pack_mountain, pack_params,
+                     pack_state)
 
 MODES = {"centralized": L.MODE_CENTRALIZED, "consensus-admm": L.MODE_CADMM, "cadmm": L.MODE_CADMM,
          "dual-decomposition": L.MODE_DD, "dd": L.MODE_DD}
@@ -183,6 +184,37 @@ class BatchedController:
         L.check(self._lib.dat_env_rows(self._h, L.ptr(lhs), L.ptr(rhs), L.ptr(nr, L.I), L.ptr(col, L.U8), L.ptr(md)))
         return lhs, rhs, nr, col.astype(bool), md
 
+    def solve_agent_qps(self, scenario, agent, acc_des, lam=None, rho=None, f_mean=None, c=None) -> dict:
+        """Raw batched agent QPs (dat_solve_agent_qp_batch): RQPPrimalSolver.solve of C-ADMM
+        (control/rqp_cadmm.py:482-501; lam, f_mean (K, 3, n), rho (K,)) or DD (control/rqp_dd.py:475-505;
+        c (K, 9) = (c_fi, c_Fi, c_Mi)) at the handle's current states.  Returns x ((K, 3, n) C-ADMM copies
+        f, or (K, 9) DD (f_i, F_i, M_i)), status, ipm_iters, collision, min_env_dist."""
+        n = self.n
+        sc, ag = L.i32(np.atleast_1d(scenario)), L.i32(np.atleast_1d(agent))
+        K = sc.shape[0]
+        acc = L.f64(acc_des).reshape(K, 6)
+        dd = self.mode == L.MODE_DD
+        if dd:
+            cc = L.f64(c).reshape(K, 9)
+            la = rh = fm = None
+            x = np.empty((K, 9))
+        else:
+            cc = None
+            la = L.f64(np.asarray(lam, float).reshape(K, 3, n).transpose(0, 2, 1).reshape(K, 3 * n))
+            fm = L.f64(np.asarray(f_mean, float).reshape(K, 3, n).transpose(0, 2, 1).reshape(K, 3 * n))
+            rh = L.f64(np.broadcast_to(np.asarray(rho, float), (K,)))
+            x = np.empty((K, 3 * n))
+        st = np.empty(K, dtype=np.int32)
+        it = np.empty(K, dtype=np.int32)
+        col = np.empty(K, dtype=np.uint8)
+        md = np.empty(K)
+        L.check(self._lib.dat_solve_agent_qp_batch(self._h, K, L.ptr(sc, L.I), L.ptr(ag, L.I), L.ptr(acc), L.ptr(la),
+                                                   L.ptr(rh), L.ptr(fm), L.ptr(cc), L.ptr(x), L.ptr(st, L.I),
+                                                   L.ptr(it, L.I), L.ptr(col, L.U8), L.ptr(md)))
+        if not dd:
+            x = x.reshape(K, n, 3).transpose(0, 2, 1)
+        return {"x": x, "status": st, "ipm_iters": it, "collision": col.astype(bool), "min_env_dist": md}
+
     def counters(self):
         """(agent-QP solves, IPM iterations, HL steps, summed HL kernel ms) since the last reset."""
         w = self.work()
@@ -277,6 +309,88 @@ class RQPDDController(_DropIn):
         self._eng.set_max_iter(max_iter)
 
 
+class _PrimalSolver:
+    """One agent's QP solver with the reference's per-call interface and status handling, solved by
+    k_agent_qp through dat_solve_agent_qp_batch.  ``idx`` is the reference's Index(i, is_leader) or a
+    plain agent number; agent 0 is the leader (control/rqp_cadmm.py:553-555; set_leader after
+    construction does not change the cost weights)."""
+
+    _mode = None
+
+    def __init__(self, params: RQPParameters, col: RQPCollision, idx: Any, state: RQPState, dt: float,
+                 env: Any = None, verbose: bool = False, device: int = 0) -> None:
+        assert params.n >= 3
+        self.n = params.n
+        self.i = int(getattr(idx, "i", idx))
+        self.verbose = verbose
+        self.params = params
+        self._eng = BatchedController(self._mode, self.n, 1, pack_params(params, col), dt=dt, device=device)
+        if env is not None:
+            self._eng.set_forests([env])
+        self.f_eq = equilibrium_forces(params)
+        self.collision, self.min_env_dist = False, col.collision_radius + 5.0
+        self._set_warm_start()
+
+    def _run(self, state, acc_des, **kw):
+        self._eng.set_state(pack_state(state)[None])
+        acc = np.concatenate([np.asarray(acc_des[0], float), np.asarray(acc_des[1], float)])[None]
+        t0 = self._eng.work()["hl_kernel_ms"]
+        r = self._eng.solve_agent_qps([0], [self.i], acc, **kw)
+        self.collision, self.min_env_dist = bool(r["collision"][0]), float(r["min_env_dist"][0])
+        if self.verbose and r["status"][0] != L.QP_OPTIMAL:
+            print(f"Problem not solved to optimality, status: {int(r['status'][0])}")
+        return r, t0
+
+
+class RQPCADMMPrimalSolver(_PrimalSolver):
+    """control/rqp_cadmm.py:26-507: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) ->
+    (f (3, n), solve_time, collision, min_env_dist).  Exception -> f_eq (:491-494); non-OPTIMAL ->
+    previous solution (:496-499).  cadmm_rho must be > 0 (at rho = 0 -- the constructor's warm-up solve,
+    :131-140 -- the copies f_j, j != i, are not unique; that solve only seeds Clarabel's warm start)."""
+
+    _mode = L.MODE_CADMM
+
+    def _set_warm_start(self) -> None:
+        self.prev_f = self.f_eq.copy()
+
+    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 1.0, f_mean=None):
+        n = self.n
+        lam = np.zeros((3, n)) if lambda_f is None else np.asarray(lambda_f, float)
+        fm = np.zeros((3, n)) if f_mean is None else np.asarray(f_mean, float)
+        r, _ = self._run(state, acc_des, lam=lam[None], rho=[cadmm_rho], f_mean=fm[None])
+        st = int(r["status"][0])
+        if st == L.QP_FAILED:
+            self.prev_f = self.f_eq.copy()
+        elif st == L.QP_OPTIMAL:
+            self.prev_f = r["x"][0].copy()
+        return self.prev_f, 0.0, self.collision, self.min_env_dist
+
+
+class RQPDDPrimalSolver(_PrimalSolver):
+    """control/rqp_dd.py:27-511: solve(state, acc_des, c_fi, c_Fi, c_Mi) -> (f_i, F_i, M_i, solve_time,
+    collision, min_env_dist).  Exception -> (f_eq,i, sum f_eq - f_eq,i, -JT^-1 hat(r_com,i) f_eq,i)
+    (:484-489); non-OPTIMAL -> previous solution."""
+
+    _mode = L.MODE_DD
+
+    def _set_warm_start(self) -> None:
+        p, i = self.params, self.i
+        self.prev_fi = self.f_eq[:, i].copy()
+        self.prev_Fi = np.sum(self.f_eq, axis=1) - self.prev_fi
+        self.prev_Mi = -p.JT_inv @ _skew(p.r_com[:, i]) @ self.prev_fi
+
+    def solve(self, state, acc_des, c_fi=np.zeros(3), c_Fi=np.zeros(3), c_Mi=np.zeros(3)):
+        c = np.concatenate([np.asarray(c_fi, float), np.asarray(c_Fi, float), np.asarray(c_Mi, float)])
+        r, _ = self._run(state, acc_des, c=c[None])
+        st = int(r["status"][0])
+        if st == L.QP_FAILED:
+            self._set_warm_start()
+        elif st == L.QP_OPTIMAL:
+            x = r["x"][0]
+            self.prev_fi, self.prev_Fi, self.prev_Mi = x[:3].copy(), x[3:6].copy(), x[6:].copy()
+        return self.prev_fi, self.prev_Fi, self.prev_Mi, 0.0, self.collision, self.min_env_dist
+
+
 class RQPClosedLoop:
     """One scenario's closed loop on the GPU (example/rqp_example.py:120-131): HL control every
     ``hl_rel_freq`` steps from the given desired accelerations, SO(3) PD low level and dynamics
@@ -303,4 +417,4 @@ class RQPClosedLoop:
 
 
 __all__ = ["BatchedController", "StepResult", "SolverStatistics", "RQPCentralizedController", "RQPCADMMController",
-           "RQPDDController", "RQPClosedLoop"]
+           "RQPDDController", "RQPClosedLoop", "RQPCADMMPrimalSolver", "RQPDDPrimalSolver"]

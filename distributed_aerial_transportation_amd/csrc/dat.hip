@@ -1095,6 +1095,93 @@ __global__ void k_env(KArgs a, double* lhs, double* rhs, int* nrow, unsigned cha
   md[t] = e.min_env_dist;
 }
 
+// ------------------------------------------------------------------------------------------------
+// raw batched agent QPs: RQPPrimalSolver.solve (control/rqp_cadmm.py:482-501, control/rqp_dd.py:475-505)
+// ------------------------------------------------------------------------------------------------
+// One lane per item (a scenario's state / parameters / forest, one agent, its own multipliers).
+// Not a hot path: the scenario data live in lane registers / scratch (PlainRef), as in k_cent.
+struct AgentQPArgs {
+  int count;
+  const int *scen, *agent;
+  const double *acc, *lam, *rho, *fbar, *c9;
+  double* x;
+  int *status, *iters;
+  unsigned char* col;
+  double* mind;
+  double* best;
+};
+
+__global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = k < q.count;
+  const int n = a.n, N3 = 3 * n;
+  const bool dd = a.dlamF != nullptr;
+  const int sc = valid ? q.scen[k] : 0, i = valid ? q.agent[k] : 0;
+  const double* prm = prm_of(a, sc);
+  const double* st = a.state + (size_t)sc * a.S;
+  QPShared S;
+  QPLane<1> P;
+  EnvRows E;
+  double Rt_all[NMAX * 9];
+  int nr = NBASE;
+  EnvOut env;
+  env.collision = 0;
+  env.min_env_dist = 0.0;
+  if (valid) {
+    for (int j = 0; j < n; ++j) make_Rt(prm + DAT_P_RCOM(n) + 3 * j, st + DAT_S_RL(n), Rt_all + 9 * j);
+    build_shared(S, prm, n, st, q.acc + (size_t)k * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, !dd);
+    if (dd) {
+      lane_dd_static(P, prm, i);
+    } else {
+      lane_cadmm_static(P, prm, i);
+    }
+    const double* trees;
+    int nt;
+    unsigned emask;
+    forest_of(a, sc, &trees, &nt);
+    double lhs[DAT_NENV][3], rhs[DAT_NENV];
+    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+    set_env_rows(P, E, S, emask, lhs, rhs);
+    nr = rows_needed(P.emask);
+    if (dd) {
+      set_dd_price(P, prm, n, i, q.c9 + (size_t)k * 9);
+    } else {
+      lane_cadmm_dynamic(P, prm, n, i, Rt_all, q.lam + (size_t)k * N3, q.fbar + (size_t)k * N3, q.rho[k]);
+    }
+  }
+  nr = wave_max(nr);
+  if (!valid) return;
+  double y[1][3], w[6];
+  const PlainRef<QPShared> shr{&S};
+  const EnvPlain er{&E};
+  const RtPtr rtr{Rt_all + 9 * i};
+  double* bst = q.best + (size_t)k * best_size(1);
+  IPMOut o = dd ? ipm_solve_rows<MODE_DD, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                             IPM_TOL)
+                : ipm_solve_rows<MODE_CADMM, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
+                                                IPM_MAX_ITER, IPM_TOL);
+  if (dd) {
+    double* xo = q.x + (size_t)k * 9;
+    for (int c = 0; c < 3; ++c) xo[c] = y[0][c];
+    for (int c = 0; c < 6; ++c) xo[3 + c] = w[c];
+  } else {
+    double* xo = q.x + (size_t)k * N3;
+    const double rho = q.rho[k];
+    for (int j = 0; j < n; ++j) {
+      if (j == i) {
+        for (int c = 0; c < 3; ++c) xo[3 * j + c] = y[0][c];
+      } else {
+        cadmm_free_block(Rt_all + 9 * j, q.lam + (size_t)k * N3 + 3 * j, q.fbar + (size_t)k * N3 + 3 * j, o.pi, rho,
+                         xo + 3 * j);
+      }
+    }
+  }
+  q.status[k] = o.status;
+  q.iters[k] = o.iters;
+  q.col[k] = (unsigned char)env.collision;
+  q.mind[k] = env.min_env_dist;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -1658,6 +1745,75 @@ int dat_env_rows(dat_handle* h, double* lhs, double* rhs, int* nrow, unsigned ch
   (void)hipFree(dn);
   (void)hipFree(dc);
   if (e != hipSuccess) return fail(std::string("dat_env_rows: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, const int* agent, const double* acc_des,
+                             const double* lam, const double* rho, const double* f_mean, const double* c9, double* x,
+                             int* status, int* ipm_iters, unsigned char* collision, double* min_env_dist) {
+  if (!h) return fail("null handle");
+  if (count < 0) return fail("dat_solve_agent_qp_batch: negative count");
+  if (count == 0) return 0;
+  if (!h->have_params) return fail("dat_solve_agent_qp_batch: params not set");
+  const int mode = h->cfg.mode, n = h->cfg.n, N3 = 3 * n;
+  if (mode == DAT_MODE_CENTRALIZED) return fail("dat_solve_agent_qp_batch: C-ADMM or DD handles only");
+  const bool dd = mode == DAT_MODE_DD;
+  if (!scenario || !agent || !acc_des || !x || !status) return fail("dat_solve_agent_qp_batch: null argument");
+  if (dd ? !c9 : (!lam || !rho || !f_mean)) return fail("dat_solve_agent_qp_batch: missing multipliers");
+  for (int k = 0; k < count; ++k) {
+    if (scenario[k] < 0 || scenario[k] >= h->cfg.batch) return fail("dat_solve_agent_qp_batch: scenario out of range");
+    if (agent[k] < 0 || agent[k] >= n) return fail("dat_solve_agent_qp_batch: agent out of range");
+    if (!dd && !(rho[k] > 0.0))
+      return fail("dat_solve_agent_qp_batch: rho must be > 0 (at rho = 0 the copies f_j, j != i, are not unique)");
+  }
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t C = count, nx = dd ? 9 : N3;
+  std::vector<void*> tmp;
+  auto dev = [&](size_t bytes, const void* src) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 8) != hipSuccess) return nullptr;
+    tmp.push_back(p);
+    if (src && hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, h->stream) != hipSuccess) return nullptr;
+    return p;
+  };
+  AgentQPArgs q;
+  memset(&q, 0, sizeof(q));
+  q.count = count;
+  q.scen = (const int*)dev(sizeof(int) * C, scenario);
+  q.agent = (const int*)dev(sizeof(int) * C, agent);
+  q.acc = (const double*)dev(sizeof(double) * C * 6, acc_des);
+  if (dd) {
+    q.c9 = (const double*)dev(sizeof(double) * C * 9, c9);
+  } else {
+    q.lam = (const double*)dev(sizeof(double) * C * N3, lam);
+    q.rho = (const double*)dev(sizeof(double) * C, rho);
+    q.fbar = (const double*)dev(sizeof(double) * C * N3, f_mean);
+  }
+  q.x = (double*)dev(sizeof(double) * C * nx, nullptr);
+  q.status = (int*)dev(sizeof(int) * C, nullptr);
+  q.iters = (int*)dev(sizeof(int) * C, nullptr);
+  q.col = (unsigned char*)dev(C, nullptr);
+  q.mind = (double*)dev(sizeof(double) * C, nullptr);
+  q.best = (double*)dev(sizeof(double) * C * best_size(1), nullptr);
+  bool ok = q.scen && q.agent && q.acc && q.x && q.status && q.iters && q.col && q.mind && q.best &&
+            (dd ? q.c9 != nullptr : (q.lam && q.rho && q.fbar));
+  hipError_t e = hipSuccess;
+  if (ok) {
+    KArgs a = kargs(h);
+    hipLaunchKernelGGL(k_agent_qp, dim3((count + 63) / 64), dim3(64), 0, h->stream, a, q);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(x, q.x, sizeof(double) * C * nx, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(status, q.status, sizeof(int) * C, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && ipm_iters) e = hipMemcpyAsync(ipm_iters, q.iters, sizeof(int) * C, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && collision) e = hipMemcpyAsync(collision, q.col, C, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && min_env_dist)
+      e = hipMemcpyAsync(min_env_dist, q.mind, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream);
+  }
+  hipError_t es = hipStreamSynchronize(h->stream);
+  for (void* p : tmp) (void)hipFree(p);
+  if (!ok) return fail("dat_solve_agent_qp_batch: device allocation failed");
+  if (e != hipSuccess) return fail(std::string("dat_solve_agent_qp_batch: ") + hipGetErrorString(e));
+  if (es != hipSuccess) return fail(std::string("dat_solve_agent_qp_batch: ") + hipGetErrorString(es));
   return 0;
 }
 

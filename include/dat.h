@@ -139,6 +139,22 @@ int dat_set_persistent_blocks(dat_handle* h, int blocks);
  * B x n x 10, nrow B x n, collision B x n, min_dist B x n (agent = -1 row when centralized). */
 int dat_env_rows(dat_handle* h, double* lhs, double* rhs, int* nrow, unsigned char* collision, double* min_dist);
 
+/* dat_solve_agent_qp_batch: `count` independent agent QPs -- RQPPrimalSolver.solve
+ *   C-ADMM handles: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) -> f   control/rqp_cadmm.py:482-501
+ *   DD handles:     solve(state, acc_des, c_fi, c_Fi, c_Mi) -> (f_i, F_i, M_i) control/rqp_dd.py:475-505
+ * at the handle's current states (dat_set_state), parameters and forests.  Item k: scenario[k],
+ * agent[k], acc_des[6k..] (dvl_des, dwl_des) and
+ *   C-ADMM: lam[3n k ..] (lambda_f, agent-major 3-vectors), rho[k] > 0, f_mean[3n k ..];
+ *   DD:     c9[9k ..] = (c_fi, c_Fi, c_Mi)  (lam, rho, f_mean unused; NULL allowed).
+ * Outputs: x[3n k ..] (C-ADMM: agent i's full copy f, agent-major) or x[9k ..] (DD: f_i, F_i, M_i),
+ * status[k] (DAT_QP_*), and, if not NULL, ipm_iters[k], collision[k], min_env_dist[k] of the agent's
+ * env query (control/rqp_cadmm.py:307-373).  A non-OPTIMAL item returns the IPM's best iterate; the
+ * reference's fallbacks (hold previous / f_eq, :491-499) are the caller's (RQP*PrimalSolver in
+ * control.py).  No warm state is read or written. */
+int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, const int* agent, const double* acc_des,
+                             const double* lam, const double* rho, const double* f_mean, const double* c9, double* x,
+                             int* status, int* ipm_iters, unsigned char* collision, double* min_env_dist);
+
 #ifdef __cplusplus
 }
 #endif

@@ -300,9 +300,58 @@ def gen_closed_loop(steps=400):
     np.savez(os.path.join(OUT, "ref_closed_loop.npz"), **out)
 
 
+LONG_T = {"centralized": 100.0, "consensus-admm": 100.0, "dual-decomposition": 10.0}
+
+
+def gen_long_closed_loop(name, T=None, state_every=10):
+    """rqp_example's main loop (example/rqp_example.py:85-131) over the reference horizon T = 100 s
+    (10 s for DD, whose reference loop takes up to 101 x 3 agent solves per step): forest seed 0,
+    n = 3, HL every 10 steps, LL "pd".  Recorded per HL step: f_des, iter, min_env_dist; per log step
+    (i % log_freq == 0, after that step's integrate, :114-120): x_err, v_err; and every
+    ``state_every``-th log step the state and the LL wrench w = (f (n), M (3, n)).  Written to
+    ref_long_<tag>.npz (compressed)."""
+    T = LONG_T[name] if T is None else T
+    np.random.seed(0)
+    env = Forest()
+    p, col, s0 = rqp_setup(3)
+    dt, hl = 1e-3, 10
+    dyn = RQPDynamics(p, s0, dt)
+    cls = {"consensus-admm": RQPCADMMController, "dual-decomposition": RQPDDController,
+           "centralized": RQPCentralizedController}[name]
+    ctl = cls(p, col, s0, dt, env)
+    ll = RQPLowLevelController("pd", p, ctl.get_force_cone_angle_bound())
+    from example.rqp_example import _desired_acceleration_forest  # noqa: E402 (matplotlib import)
+    steps = int(round(T / dt))
+    fdes, its, mds, xe, ve, xs, ws = [], [], [], [], [], [], []
+    for i in range(steps):
+        if i % hl == 0:
+            acc, x_ref, v_ref = _desired_acceleration_forest(dyn.state, i * dt, env)
+            f_des, st = ctl.control(dyn.state, acc)
+            fdes.append(f_des.copy()), its.append(st.iter), mds.append(st.min_env_dist)
+        w = ll.control(dyn.state, f_des)
+        dyn.integrate(w)
+        if i % hl == 0:
+            s = dyn.state
+            xe.append(np.linalg.norm(x_ref - s.xl)), ve.append(np.linalg.norm(v_ref - s.vl))
+            if (i // hl) % state_every == 0:
+                xs.append(np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl]))
+                ws.append(np.concatenate([np.asarray(w[0]).reshape(-1), np.asarray(w[1]).reshape(-1)]))
+        if i % 10000 == 0:
+            print(f"{name}: t = {i * dt:.0f} s", flush=True)
+    tag = name.split("-")[0][:4]
+    np.savez_compressed(os.path.join(OUT, f"ref_long_{tag}.npz"), T=T, dt=dt, hl_rel_freq=hl, state_every=state_every,
+                        f_des=np.array(fdes), iters=np.array(its, dtype=np.int16), min_dist=np.array(mds),
+                        x_err=np.array(xe), v_err=np.array(ve), states=np.array(xs), w=np.array(ws))
+
+
 if __name__ == "__main__":
     import time
 
+    if len(sys.argv) > 2 and sys.argv[1] == "long":
+        t = time.time()
+        gen_long_closed_loop(sys.argv[2])
+        print(f"gen_long_closed_loop({sys.argv[2]}): {time.time() - t:.1f}s", flush=True)
+        sys.exit(0)
     for fn in (gen_params, gen_dynamics, gen_lowlevel, gen_forest, gen_env_rows, gen_qp, gen_outer_loops,
                gen_closed_loop):
         t = time.time()

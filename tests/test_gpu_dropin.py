@@ -1,0 +1,182 @@
+"""GPU parity of the drop-in surfaces (through libdat.so):
+
+* the raw batched agent-QP entry ``dat_solve_agent_qp_batch`` -- RQPPrimalSolver.solve of C-ADMM
+  (control/rqp_cadmm.py:482-501) and DD (control/rqp_dd.py:475-505) -- against the reference's own
+  traced problems (ref_qp.npz, answered by the oracle IPM) and against the oracle on forest states
+  whose env CBF rows bind (control/rqp_cadmm.py:307-373);
+* the single-agent drop-ins ``RQPCADMMPrimalSolver`` / ``RQPDDPrimalSolver`` incl. the reference's
+  fallbacks (exception -> f_eq :491-494 / rqp_dd.py:484-489; non-OPTIMAL -> previous :496-499);
+* the drop-in controllers ``RQPCADMMController`` / ``RQPDDController`` / ``RQPCentralizedController``,
+  constructed from the package's RQPParameters / RQPCollision / RQPState and Forest.seeded(0), driven
+  through ``.control(state, acc_des)`` over the 400 ms loop of example/rqp_example.py:120-131 against
+  the reference's loop (ref_closed_loop.npz), with an independent GPU rollout between HL steps.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import controllers as oc
+from oracle import forest as of
+from oracle import model as om
+from oracle import scenarios as osc
+from oracle.ipm import OPTIMAL, solve_qp
+from tests._golden import load, state_from, unpack_flat
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _pack(s):
+    from distributed_aerial_transportation_amd import system
+
+    return system.pack_state(s)
+
+
+@pytest.mark.parametrize("kind", ["cadmm", "dd"])
+def test_gpu_agent_qp_batch_golden(kind):
+    """Six traced reference problems per kind (n = 3, agent i = case % 3), one batched call."""
+    from distributed_aerial_transportation_amd import BatchedController, scenarios
+
+    d = load("ref_qp.npz")
+    K = 6
+    states = np.stack([_pack(state_from(d, f"{kind}{k}_s_")) for k in range(K)])
+    eng = BatchedController(kind, 3, K, scenarios.params_block(3))
+    eng.set_state(states)
+    agent = [int(d[f"{kind}{k}_i"]) for k in range(K)]
+    acc = np.stack([d[f"{kind}{k}_acc"] for k in range(K)])
+    if kind == "cadmm":
+        r = eng.solve_agent_qps(np.arange(K), agent, acc, lam=np.stack([d[f"cadmm{k}_lam"] for k in range(K)]),
+                                rho=np.ones(K), f_mean=np.stack([d[f"cadmm{k}_fm"] for k in range(K)]))
+    else:
+        r = eng.solve_agent_qps(np.arange(K), agent, acc, c=np.stack([d[f"dd{k}_c"] for k in range(K)]))
+    assert np.all(r["status"] == 0)
+    for k in range(K):
+        x = d[f"{kind}{k}_x"][9:]
+        ref = x.reshape(3, 3, order="F") if kind == "cadmm" else x
+        assert _rel(r["x"][k], ref) < REL, (k, r["x"][k], ref)
+        assert 0 < r["ipm_iters"][k] <= 30
+
+
+def test_gpu_agent_qp_batch_forest_rows_bind():
+    """n = 6 C-ADMM agent QPs on near-tree forest states (env rows active) vs the oracle."""
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+    from tests.test_gpu_c4 import _oforest, near_tree_states
+
+    n, B = 6, 16
+    rng = np.random.default_rng(2024)
+    forests = [Forest.seeded(s) for s in range(4)]
+    sf = np.arange(B) % 4
+    states = near_tree_states(n, forests, sf, rng, d_axis=(1.6, 2.2))
+    eng = BatchedController("cadmm", n, B, scenarios.params_block(n))
+    eng.set_forests(forests, sf)
+    eng.set_state(states)
+    p = osc.params(n)
+    feq = om.equilibrium_forces(p)
+    c = om.Consts.make(p, osc.col_radius(n), distributed=True)
+    K = 2 * B
+    sc = np.repeat(np.arange(B), 2)
+    ag = rng.integers(0, n, K)
+    acc = np.concatenate([rng.uniform(-1, 1, (K, 3)), rng.uniform(-0.5, 0.5, (K, 3))], axis=1)
+    lam = rng.normal(0, 0.3, (K, 3, n))
+    fm = feq[None] + rng.normal(0, 0.5, (K, 3, n))
+    rho = rng.uniform(1.0, 2.0, K)
+    r = eng.solve_agent_qps(sc, ag, acc, lam=lam, rho=rho, f_mean=fm)
+    binding = 0
+    for k in range(K):
+        from distributed_aerial_transportation_amd.system import RQPState
+
+        s0 = RQPState.unpack(states[sc[k]], n)
+        s = om.State(s0.R, s0.w, s0.xl, s0.vl, s0.Rl, s0.wl, project=False)
+        env = of.env_rows(_oforest(forests[sf[sc[k]]]), c, s, osc.col_radius(n), p.r[:, ag[k]])
+        assert bool(r["collision"][k]) == bool(env.collision)
+        assert r["min_env_dist"][k] == pytest.approx(env.min_env_dist, abs=1e-8)
+        P, q, G, h, dims, A, b = om.build_qp("cadmm", p, c, s, (acc[k, :3], acc[k, 3:]), env, i=int(ag[k]), f_eq=feq,
+                                             lam=lam[k], rho=rho[k], f_mean=fm[k])
+        ro = solve_qp(P, q, G, h, dims, A, b)
+        assert ro.status == OPTIMAL and r["status"][k] == 0
+        ref = ro.x[9:].reshape(3, n, order="F")
+        assert _rel(r["x"][k], ref) < REL, (k, _rel(r["x"][k], ref))
+        on = np.any(env.lhs != 0.0, axis=1)
+        if np.any(on):  # an env row binds: lhs . dvl - rhs = 0 at the minimiser (dvl = x[3:6])
+            binding += int(np.min(env.lhs[on] @ ro.x[3:6] - env.rhs[on]) < 1e-7)
+    assert binding >= 3, binding  # env rows are active in a fair share of the solves
+
+
+def test_gpu_primal_solver_dropins_and_fallbacks():
+    """RQPCADMMPrimalSolver / RQPDDPrimalSolver: traced golden solves, then the fallbacks."""
+    from distributed_aerial_transportation_amd import RQPCADMMPrimalSolver, RQPDDPrimalSolver, scenarios, system
+
+    d = load("ref_qp.npz")
+    p, col, _ = scenarios.rqp_setup(3)
+    feq = system.equilibrium_forces(p)
+    for k in range(6):
+        s = system.RQPState.unpack(_pack(state_from(d, f"cadmm{k}_s_")), 3)
+        acc = (d[f"cadmm{k}_acc"][:3], d[f"cadmm{k}_acc"][3:])
+        ps = RQPCADMMPrimalSolver(p, col, int(d[f"cadmm{k}_i"]), s, 1e-3)
+        f, t, coll, md = ps.solve(s, acc, d[f"cadmm{k}_lam"], 1.0, d[f"cadmm{k}_fm"])
+        assert _rel(f, d[f"cadmm{k}_x"][9:].reshape(3, 3, order="F")) < REL
+        # payload upside down: the tilt CBF row 0 . dwl >= cos 15 deg - Rl[2,2] > 0 is infeasible -> hold
+        bad = system.RQPState.unpack(_pack(state_from(d, f"cadmm{k}_s_")), 3)
+        bad.Rl = np.diag([1.0, -1.0, -1.0])
+        bad.wl = np.zeros(3)
+        f2, *_ = ps.solve(bad, acc, d[f"cadmm{k}_lam"], 1.0, d[f"cadmm{k}_fm"])
+        assert np.array_equal(f2, f)
+        # NaN state: the solver fails (the reference's exception branch) -> f_eq
+        nan = system.RQPState.unpack(_pack(state_from(d, f"cadmm{k}_s_")), 3)
+        nan.vl = np.full(3, np.nan)
+        f3, *_ = ps.solve(nan, acc, d[f"cadmm{k}_lam"], 1.0, d[f"cadmm{k}_fm"])
+        assert np.array_equal(f3, feq)
+    for k in range(6):
+        s = system.RQPState.unpack(_pack(state_from(d, f"dd{k}_s_")), 3)
+        acc = (d[f"dd{k}_acc"][:3], d[f"dd{k}_acc"][3:])
+        i = int(d[f"dd{k}_i"])
+        ps = RQPDDPrimalSolver(p, col, i, s, 1e-3)
+        cc = d[f"dd{k}_c"]
+        fi, Fi, Mi, t, coll, md = ps.solve(s, acc, cc[:3], cc[3:6], cc[6:])
+        assert _rel(np.concatenate([fi, Fi, Mi]), d[f"dd{k}_x"][9:]) < REL
+        nan = system.RQPState.unpack(_pack(state_from(d, f"dd{k}_s_")), 3)
+        nan.vl = np.full(3, np.nan)
+        fi, Fi, Mi, *_ = ps.solve(nan, acc, cc[:3], cc[3:6], cc[6:])
+        np.testing.assert_array_equal(fi, feq[:, i])
+        np.testing.assert_allclose(Fi, feq.sum(axis=1) - feq[:, i], rtol=0, atol=1e-15)
+        np.testing.assert_allclose(Mi, -p.JT_inv @ system._skew(p.r_com[:, i]) @ feq[:, i], rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("tag,name", [("cons", "RQPCADMMController"), ("dual", "RQPDDController"),
+                                      ("cent", "RQPCentralizedController")])
+def test_gpu_dropin_controller_closed_loop(tag, name):
+    """The reference's loop with the drop-in controller: acc_des from the forest law on the host,
+    ctl.control(state, acc) per HL step, 10 simulation steps on a separate GPU dynamics engine."""
+    import distributed_aerial_transportation_amd as dat
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios, system
+
+    d = load("ref_closed_loop.npz")
+    p, col, s = scenarios.rqp_setup(3)
+    forest = Forest.seeded(0)
+    ctl = getattr(dat, name)(p, col, s, 1e-3, forest)
+    assert ctl.get_force_cone_angle_bound() == pytest.approx(np.pi / 6)
+    assert ctl.get_dist_eps() == pytest.approx(0.1)
+    sim = BatchedController("cadmm", 3, 1, system.pack_params(p, col))
+    sim.set_state(system.pack_state(s)[None], np.zeros(1, dtype=np.int32))
+    steps = d[f"{tag}_states"].shape[0] // 10
+    for k in range(steps):
+        x, _ = sim.get_state()
+        st = system.RQPState.unpack(x[0], 3)
+        acc, _, _ = oc.desired_acceleration_forest(om.State(st.R, st.w, st.xl, st.vl, st.Rl, st.wl, project=False),
+                                                   forest)
+        f, stats = ctl.control(st, acc)
+        assert _rel(f, d[f"{tag}_f_des"][k]) < REL, k
+        if tag != "cent":
+            assert stats.iter == d[f"{tag}_iters"][k]
+        else:
+            assert stats.iter == -1
+        assert stats.min_env_dist == pytest.approx(float(d[f"{tag}_min_dist"][k]), abs=1e-8)
+        sim.rollout(10, f[None])
+        x, _ = sim.get_state()
+        ref = system.pack_state(unpack_flat(d[f"{tag}_states"][10 * k + 9], 3))
+        assert np.max(np.abs(x[0] - ref)) < 1e-4, k
