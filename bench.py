@@ -127,36 +127,51 @@ def cpu_baseline_qp(cfg: str, n: int, mode: str, budget_s: float, fixed_work: bo
                       f"{solves} agent QPs in {dt:.1f} s"}
 
 
-def cpu_baseline(n: int, budget_s: float, start: str = "path"):
-    """Oracle (numpy) C-ADMM on a bounded sample of the same workload, one core."""
+def cpu_baseline(n: int, budget_s: float, start: str = "path", forests_n: int = 64):
+    """The C4 closed loop on this host's cores (cpu_baseline/: the same per-scenario C-ADMM loop and
+    per-lane fp64 code as the GPU, OpenMP over scenarios, -O3 x86-64-v3) on a bounded sample of the
+    same workload: rank 0's start states, 2 untimed warm-up HL steps, then timed HL steps (desired
+    acceleration + C-ADMM control + 10 simulation steps) until the time budget is spent; once on
+    all OpenMP threads (the reported value) and once on 1 thread."""
+    import cpu_baseline as cb
     from distributed_aerial_transportation_amd import Forest, scenarios
-    from distributed_aerial_transportation_amd.system import RQPState
-    from oracle import controllers as oc
-    from oracle import forest as of
-    from oracle import model as om
-    from oracle import scenarios as osc
 
-    rng = np.random.default_rng(123)
-    np.random.seed(0)
-    forest = of.Forest()
-    layout = Forest.seeded(0)  # the same seed-0 tree layout, with the terrain helper for the start heights
-    solves, t0, steps = 0, time.perf_counter(), 0
-    while time.perf_counter() - t0 < budget_s:
-        if start == "path":
-            x = scenarios.forest_path_states(n, 1, rng, [layout], np.zeros(1, dtype=int))[0]
-        else:
-            x = scenarios.forest_start_states(n, 1, rng)[0]
-        s = RQPState.unpack(x, n)
-        st = om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
-        ctl = oc.CADMM(osc.params(n), osc.col_radius(n), forest)
-        acc, _, _ = oc.desired_acceleration_forest(st, forest)
-        _, stats = ctl.control(st, acc)
-        solves += stats.iter * n
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
-            "sample": f"oracle C-ADMM n={n} (numpy dense IPM), {steps} forest control steps from C4 start "
-                      f"states ({start} start), {solves} agent QPs in {dt:.1f} s"}
+    cb.build()
+    threads = cb.CpuClosedLoop.max_threads()
+    S = max(256, 64 * threads)
+    scen_forest, seed = shard(0, S, forests_n)
+    rng = np.random.default_rng(seed)
+    forests = [Forest.seeded(s) for s in range(forests_n)]
+    if start == "path":
+        states = scenarios.forest_path_states(n, S, rng, forests, scen_forest)
+    else:
+        states = scenarios.forest_start_states(n, S, rng)
+
+    def run(nthreads, count, budget):
+        c = cb.CpuClosedLoop(n, S, scenarios.params_block(n))
+        c.set_forests(forests, scen_forest)
+        c.set_state(states)
+        c.closed_loop(2, count=count, threads=nthreads)  # warm-up: the GPU bench times warm steps too
+        q = ipm = steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            dq, di = c.closed_loop(1, count=count, threads=nthreads)
+            q, ipm, steps = q + dq, ipm + di, steps + 1
+        return q / (time.perf_counter() - t0), q, ipm, steps
+
+    v1, q1, _, st1 = run(1, min(S, 64), 0.25 * budget_s)
+    vN, qN, iN, stN = run(threads, S, 0.75 * budget_s)
+    try:
+        cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except (OSError, IndexError):
+        cpu = "unknown"
+    return {"value": vN, "unit": "agent-QP solves/s", "cores": threads, "kind": "port",
+            "single_core_value": v1,
+            "sample": f"C++ OpenMP restatement of the C4 loop (cpu_baseline/dat_cpu.hip, same per-lane code as the "
+                      f"kernels), n={n}, {S} of the bench's {start}-start scenarios, {stN} warm HL steps "
+                      f"({qN} agent QPs, {iN / max(qN, 1):.2f} IPM it/QP) on {threads} threads; 1 thread: "
+                      f"{min(S, 64)} scenarios x {st1} steps ({q1} QPs); host CPU {cpu}, os.cpu_count() "
+                      f"{os.cpu_count()}"}
 
 
 def shard(rank: int, batch: int, num_forests: int):

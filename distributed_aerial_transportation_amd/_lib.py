@@ -118,10 +118,11 @@ def lib() -> ctypes.CDLL:
     """Load libdat.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get("DAT_LIB_PATH", LIB_PATH)  # development: A/B a differently compiled build
+        if not os.path.exists(path):
             raise DatError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
                            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         for name, (res, args) in EXPORTS.items():
             f = getattr(L, name)
             f.restype = res

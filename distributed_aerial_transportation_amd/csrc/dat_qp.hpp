@@ -67,7 +67,9 @@ struct LdsRef {
   int idx;
   __device__ const T& get() const {
     int j = idx;
+#ifndef DAT_LDS_HOIST
     __asm__ volatile("" : "+v"(j));
+#endif
     return base[j];
   }
 };
@@ -87,12 +89,16 @@ struct EnvLds {
   int lane;
   __device__ double a(int j, int c) const {
     int l = lane;
+#ifndef DAT_LDS_HOIST
     __asm__ volatile("" : "+v"(l));
+#endif
     return base[(3 * j + c) * 64 + l];
   }
   __device__ double b(int j) const {
     int l = lane;
+#ifndef DAT_LDS_HOIST
     __asm__ volatile("" : "+v"(l));
+#endif
     return base[(3 * DAT_NENV + j) * 64 + l];
   }
 };
@@ -115,7 +121,9 @@ struct RtLds {
   int off;  // offset of block 0 in doubles
   __device__ const double* get(int k) const {
     int j = off;
+#ifndef DAT_LDS_HOIST
     __asm__ volatile("" : "+v"(j));
+#endif
     return base + j + 9 * k;
   }
 };
