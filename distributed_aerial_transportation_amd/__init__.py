@@ -13,7 +13,7 @@ from .system import RQPCollision, RQPParameters, RQPState, pack_params, pack_sta
 def __getattr__(name):
     # controllers load libdat.so lazily so that data-only imports work without a GPU
     if name in ("BatchedController", "RQPCentralizedController", "RQPCADMMController", "RQPDDController",
-                "RQPClosedLoop", "SolverStatistics", "StepResult", "RQPCADMMPrimalSolver", "RQPDDPrimalSolver"):
+                "RQPClosedLoop", "SolverStatistics", "StepResult", "RQPCADMMPrimalSolver", "RQPDDPrimalSolver", "RQPLowLevelController"):
         from . import control
 
         return getattr(control, name)

@@ -23,6 +23,7 @@ DEPS = [SRC, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc"
 
 MODE_CENTRALIZED, MODE_CADMM, MODE_DD = 0, 1, 2
 QP_OPTIMAL, QP_INACCURATE, QP_INFEASIBLE, QP_FAILED = 0, 1, 2, 3
+LL_KINDS = {"pd": 0, "sm": 1}
 
 
 class DatError(RuntimeError):
@@ -111,6 +112,8 @@ EXPORTS = {
     "dat_set_persistent_blocks": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_env_rows": (ctypes.c_int, [H, D, D, I, U8, D]),
     "dat_solve_agent_qp_batch": (ctypes.c_int, [H, ctypes.c_int, I, I, D, D, D, D, D, D, I, I, U8, D]),
+    "dat_set_low_level": (ctypes.c_int, [H, ctypes.c_int]),
+    "dat_low_level_control": (ctypes.c_int, [H, D, D, D]),
 }
 
 

@@ -12,7 +12,9 @@ Drop-in single-scenario classes (same constructor and per-step interface as the 
         ``control(state, acc_des) -> (f_des (3, n), SolverStatistics)``,
         ``get_force_cone_angle_bound()``, ``get_dist_eps()``,
         ``set_force_err_tolerance(tol[, use_total_res])``, ``set_max_iter(k)`` (C-ADMM / DD).
-  ``RQPLowLevelController`` / ``RQPDynamics``: low-level PD + rigid-body rollout on the GPU.
+  ``RQPLowLevelController(so3_controller_type, params, max_f_ang)``: control/rqp_centralized.py:457-535
+        ("pd" or "sm" SO(3) law) on the GPU; ``BatchedController.set_low_level`` selects the law of the
+        device rollout (SO(3) law + rigid-body dynamics + Lie integration).
 The QPs are solved by the HIP kernels; the reference's Clarabel per-call solve time becomes the
 GPU kernel time of the step (``SolverStatistics.solve_time``).
 """
@@ -164,6 +166,23 @@ class BatchedController:
                                            L.ptr(md), L.ptr(col, L.U8), L.ptr(err)))
         _, _, _, ms1 = self.counters()
         return StepResult(f.reshape(B, n, 3).transpose(0, 2, 1), it, qs, md, col.astype(bool), err, ms1 - ms0)
+
+    def set_low_level(self, so3_controller_type: str) -> None:
+        """Low-level law of rollout / closed_loop: "pd" (default) or "sm" (control/rqp_centralized.py:468-482)."""
+        if so3_controller_type not in L.LL_KINDS:
+            raise NotImplementedError(so3_controller_type)
+        L.check(self._lib.dat_set_low_level(self._h, L.LL_KINDS[so3_controller_type]))
+
+    def low_level(self, f_des: Optional[np.ndarray] = None):
+        """RQPLowLevelController.control at the current states: (thrust (B, n), moment (B, 3, n))."""
+        B, n = self.batch, self.n
+        fd = None
+        if f_des is not None:
+            fd = L.f64(np.asarray(f_des, float).reshape(B, 3, n).transpose(0, 2, 1).reshape(B, 3 * n))
+        f = np.empty((B, n))
+        M = np.empty((B, n, 3))
+        L.check(self._lib.dat_low_level_control(self._h, L.ptr(fd), L.ptr(f), L.ptr(M)))
+        return f, M.transpose(0, 2, 1)
 
     def rollout(self, steps: int, f_des: Optional[np.ndarray] = None) -> None:
         fd = None
@@ -391,6 +410,29 @@ class RQPDDPrimalSolver(_PrimalSolver):
         return self.prev_fi, self.prev_Fi, self.prev_Mi, 0.0, self.collision, self.min_env_dist
 
 
+class RQPLowLevelController:
+    """control/rqp_centralized.py:457-535: RQPLowLevelController(so3_controller_type, params, max_f_ang)
+    .control(state, f_des) -> (f (n,), M (3, n)); "pd" or "sm" SO(3) law, evaluated on the GPU
+    (k_low_level).  Unknown types raise NotImplementedError like the reference (:483-484)."""
+
+    def __init__(self, so3_controller_type: str, params: RQPParameters, max_f_ang: float, device: int = 0) -> None:
+        if so3_controller_type not in L.LL_KINDS:
+            raise NotImplementedError(so3_controller_type)
+        self.n = params.n
+        self.cos_max_f_ang = np.cos(max_f_ang)
+        col = RQPCollision(np.zeros((1, 3)), np.zeros((1, 3)))  # the LL law reads only J
+        self._eng = BatchedController(L.MODE_CADMM, self.n, 1, pack_params(params, col), device=device)
+        self._eng.set_low_level(so3_controller_type)
+
+    def control(self, state, f_des: np.ndarray):
+        f_des = np.asarray(f_des, float)
+        assert f_des.shape == (3, state.n)
+        assert all(f_des[2, :] > 0.0)
+        self._eng.set_state(pack_state(state)[None])
+        f, M = self._eng.low_level(f_des[None])
+        return f[0], M[0]
+
+
 class RQPClosedLoop:
     """One scenario's closed loop on the GPU (example/rqp_example.py:120-131): HL control every
     ``hl_rel_freq`` steps from the given desired accelerations, SO(3) PD low level and dynamics
@@ -417,4 +459,4 @@ class RQPClosedLoop:
 
 
 __all__ = ["BatchedController", "StepResult", "SolverStatistics", "RQPCentralizedController", "RQPCADMMController",
-           "RQPDDController", "RQPClosedLoop", "RQPCADMMPrimalSolver", "RQPDDPrimalSolver"]
+           "RQPDDController", "RQPClosedLoop", "RQPCADMMPrimalSolver", "RQPDDPrimalSolver", "RQPLowLevelController"]

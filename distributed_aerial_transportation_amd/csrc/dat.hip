@@ -98,6 +98,7 @@ struct KArgs {
   double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
                                  //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
   unsigned* emask;               // C-ADMM: [B n] env row mask of the step
+  int ll_kind;                   // low-level SO(3) law: LL_PD or LL_SM (dat_set_low_level)
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)
@@ -1001,7 +1002,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArgs a, int steps, double dt, c
   for (int k = 0; k < S; ++k) st[k] = g[k];
   int cnt = a.counter[sc];
   const double* fd = fdes + (size_t)sc * 3 * n;
-  for (int s = 0; s < steps; ++s) sim_step<NA>(prm, n, st, &cnt, fd, dt);
+  for (int s = 0; s < steps; ++s) sim_step<NA>(prm, n, st, &cnt, fd, dt, a.ll_kind);
   for (int k = 0; k < S; ++k) g[k] = st[k];
   a.counter[sc] = cnt;
 }
@@ -1014,6 +1015,19 @@ void launch_rollout(const KArgs& a, int B, hipStream_t stream, int steps, double
     hipLaunchKernelGGL(k_rollout<6>, grid, block, 0, stream, a, steps, dt, fdes);
   else
     hipLaunchKernelGGL(k_rollout<0>, grid, block, 0, stream, a, steps, dt, fdes);
+}
+
+// RQPLowLevelController.control (control/rqp_centralized.py:518-535) at the current states: thrust
+// f (B x n) and moments M (B x n x 3) from f_des, one lane per (scenario, agent)
+__global__ void k_low_level(KArgs a, const double* fdes, double* fo, double* Mo) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.n;
+  if (t >= a.B * n) return;
+  const int sc = t / n, i = t - sc * n;
+  const double* prm = prm_of(a, sc);
+  const double* st = a.state + (size_t)sc * a.S;
+  ll_control_agent(st + DAT_S_R(n) + 9 * i, st + DAT_S_W(n) + 3 * i, prm + DAT_P_J(n) + 9 * i,
+                   fdes + (size_t)sc * 3 * n + 3 * i, fo + t, Mo + 3 * (size_t)t, a.ll_kind);
 }
 
 __global__ void k_desired(KArgs a, double* acc) {
@@ -1218,6 +1232,7 @@ struct dat_handle {
   unsigned* emask = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
+  int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
 };
 
@@ -1287,6 +1302,7 @@ KArgs kargs(dat_handle* h) {
   a.slist = h->slist;
   a.scount = h->scount;
   a.qhead = h->scount ? h->scount + 2 * NCLS : nullptr;
+  a.ll_kind = h->ll_kind;
   return a;
 }
 
@@ -1814,6 +1830,37 @@ int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, cons
   if (!ok) return fail("dat_solve_agent_qp_batch: device allocation failed");
   if (e != hipSuccess) return fail(std::string("dat_solve_agent_qp_batch: ") + hipGetErrorString(e));
   if (es != hipSuccess) return fail(std::string("dat_solve_agent_qp_batch: ") + hipGetErrorString(es));
+  return 0;
+}
+
+int dat_set_low_level(dat_handle* h, int kind) {
+  if (!h) return fail("null handle");
+  if (kind != DAT_LL_PD && kind != DAT_LL_SM) return fail("dat_set_low_level: kind must be DAT_LL_PD or DAT_LL_SM");
+  h->ll_kind = kind;
+  return 0;
+}
+
+int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, double* moment) {
+  if (!h || !thrust || !moment) return fail("dat_low_level_control: null argument");
+  if (!h->have_params) return fail("dat_low_level_control: params not set");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n;
+  if (f_des) HIPCHK(hipMemcpyAsync(h->fdes, f_des, sizeof(double) * B * 3 * n, hipMemcpyHostToDevice, h->stream));
+  double *df = nullptr, *dm = nullptr;
+  HIPCHK(hipMalloc(&df, sizeof(double) * B * n));
+  if (hipMalloc(&dm, sizeof(double) * B * n * 3) != hipSuccess) {
+    (void)hipFree(df);
+    return fail("dat_low_level_control: hipMalloc failed");
+  }
+  KArgs a = kargs(h);
+  hipLaunchKernelGGL(k_low_level, dim3((B * n + 63) / 64), dim3(64), 0, h->stream, a, (const double*)h->fdes, df, dm);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(thrust, df, sizeof(double) * B * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(moment, dm, sizeof(double) * B * n * 3, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  (void)hipFree(df);
+  (void)hipFree(dm);
+  if (e != hipSuccess) return fail(std::string("dat_low_level_control: ") + hipGetErrorString(e));
   return 0;
 }
 

@@ -585,11 +585,22 @@ DAT_HD void rot_from_unit(const double* q, double* R) {
   R[2] = q[0]; R[5] = q[1]; R[8] = q[2];
 }
 
-// SO(3) PD law with wd = dwd = 0 (utils/so3_tracking_controllers.py:18-43, gains
-// control/rqp_centralized.py:488-489): M = -kR e_R - kW w + w x J w, e_R = vee(Rd'R - R'Rd)/2;
-// thrust f = f_des . R e3 (control/rqp_centralized.py:527).
+// Low-level SO(3) attitude laws of RQPLowLevelController (control/rqp_centralized.py:457-535), both
+// with wd = dwd = 0 (:530-532); thrust f = f_des . R e3 (:525), Rd from f_des / |f_des| (:527-528).
+constexpr int LL_PD = 0;  // so3_pd_tracking_control (utils/so3_tracking_controllers.py:18-43)
+constexpr int LL_SM = 1;  // so3_sm_tracking_control (utils/so3_tracking_controllers.py:52-95)
+
+// sign(y) |y|^r with sign(0) = 0 (np.power(np.abs(y), r) * np.sign(y))
+DAT_HD double spow(double y, double r) { return y > 0.0 ? pow(y, r) : (y < 0.0 ? -pow(-y, r) : 0.0); }
+
+// PD (gains control/rqp_centralized.py:488-489): M = -kR e_R - kW w + w x J w, e_R = vee(Rd'R - R'Rd)/2.
+// SM (gains :491-496: r 0.5, k_R 1.415, l_R 0.707, k_s 0.113, l_s 0.057), Lee 2018 eqs. (34)-(36):
+//   s = e_W + k_R e_R + l_R S(r, e_R),  E = (tr(R'Rd) I - R'Rd) / 2,  e_W = w,
+//   M = -k_s s - l_s S(r, s) + w x J w - (k_R J + l_s r J T) E e_W,
+// with T exactly as the reference evaluates it: the call T(e_R, r) (:92) swaps the arguments of
+// T = lambda r, y: diag((|y| + 1e-6)^(r - 1)) (:88), so T = diag((0.5 + 1e-6)^(e_R,k - 1)).
 DAT_HD void ll_control_agent(const double* R, const double* w, const double* J, const double* fdes, double* f,
-                             double* M) {
+                             double* M, int kind = LL_PD) {
   *f = fdes[0] * R[2] + fdes[1] * R[5] + fdes[2] * R[8];
   double nn = sqrt(dot3(fdes, fdes));
   double qd[3] = {fdes[0] / nn, fdes[1] / nn, fdes[2] / nn};
@@ -603,6 +614,21 @@ DAT_HD void ll_control_agent(const double* R, const double* w, const double* J, 
   double Jw[3], wJw[3];
   mv3(J, w, Jw);
   cross3(w, Jw, wJw);
+  if (kind == LL_SM) {
+    const double r = 0.5, kR = 1.415, lR = 0.707, ks = 0.113, ls = 0.057, eps = 1e-6;
+    double sv[3];
+    for (int c = 0; c < 3; ++c) sv[c] = w[c] + kR * eR[c] + lR * spow(eR[c], r);
+    // E e_W with R'Rd = A'
+    const double tr = A[0] + A[4] + A[8];
+    double Ew[3];
+    for (int c = 0; c < 3; ++c) Ew[c] = 0.5 * (tr * w[c] - (A[c] * w[0] + A[3 + c] * w[1] + A[6 + c] * w[2]));
+    // (k_R J + l_s r J T) Ew = J (k_R Ew + l_s r T Ew)
+    double v[3], Jv[3];
+    for (int c = 0; c < 3; ++c) v[c] = kR * Ew[c] + ls * r * pow(r + eps, eR[c] - 1.0) * Ew[c];
+    mv3(J, v, Jv);
+    for (int c = 0; c < 3; ++c) M[c] = -ks * sv[c] - ls * spow(sv[c], r) + wJw[c] - Jv[c];
+    return;
+  }
   const double kR = 0.25, kW = 0.075;
   for (int c = 0; c < 3; ++c) M[c] = -kR * eR[c] - kW * w[c] + wJw[c];
 }
@@ -610,7 +636,8 @@ DAT_HD void ll_control_agent(const double* R, const double* w, const double* J, 
 // One simulation step of one scenario: LL control from f_des, forward dynamics, integration
 // (system/rigid_quadrotor_payload.py:173-222, 129-148).  counter: steps since the last projection.
 template <int NMAX>
-DAT_HD void sim_step(const double* prm, int n, double* st, int* counter, const double* fdes, double dt) {
+DAT_HD void sim_step(const double* prm, int n, double* st, int* counter, const double* fdes, double dt,
+                     int ll_kind = LL_PD) {
   double* R = st + DAT_S_R(n);
   double* W = st + DAT_S_W(n);
   double* xl = st + DAT_S_XL(n);
@@ -628,7 +655,7 @@ DAT_HD void sim_step(const double* prm, int n, double* st, int* counter, const d
   double dw[NMAX][3];
   for (int i = 0; i < n; ++i) {
     double f, M[3];
-    ll_control_agent(R + 9 * i, W + 3 * i, J + 9 * i, fdes + 3 * i, &f, M);
+    ll_control_agent(R + 9 * i, W + 3 * i, J + 9 * i, fdes + 3 * i, &f, M, ll_kind);
     double Jw[3], wJw[3], t[3];
     mv3(J + 9 * i, W + 3 * i, Jw);
     cross3(W + 3 * i, Jw, wJw);

@@ -26,6 +26,11 @@ extern "C" {
 #define DAT_MODE_CADMM 1       /* RQPCADMMController         control/rqp_cadmm.py:510-688    */
 #define DAT_MODE_DD 2          /* RQPDDController            control/rqp_dd.py:558-764       */
 
+/* low-level SO(3) attitude law of RQPLowLevelController(so3_controller_type, ...)
+ * (control/rqp_centralized.py:457-484) */
+#define DAT_LL_PD 0 /* "pd": so3_pd_tracking_control  utils/so3_tracking_controllers.py:18-43 */
+#define DAT_LL_SM 1 /* "sm": so3_sm_tracking_control  utils/so3_tracking_controllers.py:52-95 */
+
 /* per agent-QP status (maps the cvxpy/Clarabel outcomes the reference branches on) */
 #define DAT_QP_OPTIMAL 0    /* accepted                         (prob.status == OPTIMAL)        */
 #define DAT_QP_INACCURATE 1 /* previous solution held           (non-OPTIMAL status)            */
@@ -104,6 +109,13 @@ int dat_control_step(dat_handle* h, const double* state, const double* acc_des, 
  * RQPDynamics.integrate (system/rigid_quadrotor_payload.py:271-276) per simulation step.
  * f_des: B x 3n held constant over the steps, or NULL to use the last control step's output. */
 int dat_rollout(dat_handle* h, int steps, const double* f_des);
+/* Low-level law used by dat_rollout / dat_closed_loop: DAT_LL_PD (default, example/rqp_example.py:113)
+ * or DAT_LL_SM -- the so3_controller_type argument of RQPLowLevelController (control/rqp_centralized.py:468-482). */
+int dat_set_low_level(dat_handle* h, int kind);
+/* RQPLowLevelController.control(state, f_des) -> (f, M) (control/rqp_centralized.py:518-535) at the
+ * current states: f_des B x 3n (agent-major) or NULL (the last control step's output); thrust B x n,
+ * moment B x n x 3 (agent-major 3-vectors). */
+int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, double* moment);
 
 /* ---- device-resident closed loop (the loop of example/rqp_example.py:120-131 with the desired
  * acceleration of :33-59): hl_steps x (desired acceleration + control step +

@@ -184,9 +184,26 @@ def rotation_from_unit_vector(q):
 K_R_PD, K_OMEGA_PD = 0.25, 0.075  # control/rqp_centralized.py:488-489
 
 
-def low_level_control(p: Params, s: State, f_des):
-    """RQPLowLevelController.control with the 'pd' SO(3) law, wd = dwd = 0
-    (control/rqp_centralized.py:518-535, utils/so3_tracking_controllers.py:18-43)."""
+SM_R, SM_K_R, SM_L_R, SM_K_S, SM_L_S = 0.5, 1.415, 0.707, 0.113, 0.057  # control/rqp_centralized.py:491-496
+
+
+def so3_sm(R, Rd, w, J):
+    """so3_sm_tracking_control with wd = dwd = 0 (utils/so3_tracking_controllers.py:52-95), including
+    the reference's call T(e_R, r) (:92) against the definition T = lambda r, y (:87-88): the diagonal
+    is (|r| + 1e-6)^(e_R - 1), i.e. the arguments are swapped relative to the paper."""
+    e_R = 0.5 * unskew(Rd.T @ R - R.T @ Rd)
+    e_W = w
+    E = 0.5 * (np.trace(R.T @ Rd) * np.eye(3) - R.T @ Rd)
+    S = lambda r, y: np.power(np.abs(y), r) * np.sign(y)  # noqa: E731
+    s = e_W + SM_K_R * e_R + SM_L_R * S(SM_R, e_R)
+    T = lambda r, y: np.diag(np.power(np.abs(y) + 1e-6, r - 1))  # noqa: E731
+    return (-SM_K_S * s - SM_L_S * S(SM_R, s) + np.cross(w, J @ w)
+            - (SM_K_R * J + SM_L_S * SM_R * (J @ T(e_R, SM_R))) @ E @ e_W)
+
+
+def low_level_control(p: Params, s: State, f_des, kind: str = "pd"):
+    """RQPLowLevelController.control with the 'pd' (utils/so3_tracking_controllers.py:18-43) or 'sm'
+    (:52-95) SO(3) law, wd = dwd = 0 (control/rqp_centralized.py:518-535)."""
     n = p.n
     f = np.zeros(n)
     M = np.zeros((3, n))
@@ -196,6 +213,9 @@ def low_level_control(p: Params, s: State, f_des):
         Rd = rotation_from_unit_vector(qd)
         R = s.R[:, :, i]
         w = s.w[:, i]
+        if kind == "sm":
+            M[:, i] = so3_sm(R, Rd, w, p.J[:, :, i])
+            continue
         e_R = 0.5 * unskew(Rd.T @ R - R.T @ Rd)
         M[:, i] = -K_R_PD * e_R - K_OMEGA_PD * w + np.cross(w, p.J[:, :, i] @ w)
     return f, M

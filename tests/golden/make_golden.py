@@ -21,6 +21,11 @@ What each fixture pins (reference file:line):
   ref_dd.npz          RQPDDController.control sequences             control/rqp_dd.py:695-752
   ref_central.npz     RQPCentralizedController.control              control/rqp_centralized.py:436-448
   ref_closed_loop.npz rqp_example-style closed loop (HL every 10)   example/rqp_example.py:120-131
+  ref_lowlevel_sm.npz RQPLowLevelController("sm").control          utils/so3_tracking_controllers.py:52-95
+  ref_closed_loop_sm.npz  400 ms centralized loop with the "sm" law  control/rqp_centralized.py:474-478
+  ref_long_<tag>.npz  rqp_example over the reference horizon (100 s; DD 10 s): f_des, iters, min_dist per HL
+                      step, x_err / v_err per log step, states + LL wrench every 10th log step
+                      (python -O make_golden.py long <controller_type>)
 """
 
 from __future__ import annotations
@@ -130,18 +135,41 @@ def gen_dynamics():
     np.savez(os.path.join(OUT, "ref_dynamics.npz"), **out)
 
 
-def gen_lowlevel():
+def gen_lowlevel(kind="pd", name="ref_lowlevel.npz"):
     rng = np.random.default_rng(11)
     p, _, _ = rqp_setup(3)
-    ll = RQPLowLevelController("pd", p, np.pi / 6)
+    ll = RQPLowLevelController(kind, p, np.pi / 6)
     states, fdes, fs, Ms = [], [], [], []
     for _ in range(16):
         s = rand_state(rng, 3, big=True)
         fd = np.vstack([rng.uniform(-2, 2, (2, 3)), rng.uniform(3, 8, (1, 3))])
         f, M = ll.control(s, fd)
         states.append(pack_state(s)), fdes.append(fd), fs.append(f), Ms.append(M)
-    np.savez(os.path.join(OUT, "ref_lowlevel.npz"), **{f"s_{k}": v for k, v in stack_states(states).items()},
+    np.savez(os.path.join(OUT, name), **{f"s_{k}": v for k, v in stack_states(states).items()},
              f_des=np.array(fdes), f=np.array(fs), M=np.array(Ms))
+
+
+def gen_lowlevel_sm():
+    """RQPLowLevelController("sm") (control/rqp_centralized.py:474-478, utils/so3_tracking_controllers.py:52-95)
+    on the same states, plus a 400 ms rqp_example loop (centralized HL, forest seed 0) with the "sm" law."""
+    gen_lowlevel("sm", "ref_lowlevel_sm.npz")
+    np.random.seed(0)
+    env = Forest()
+    p, col, s0 = rqp_setup(3)
+    dyn = RQPDynamics(p, s0, 1e-3)
+    hl = RQPCentralizedController(p, col, s0, 1e-3, env)
+    ll = RQPLowLevelController("sm", p, hl.get_force_cone_angle_bound())
+    from example.rqp_example import _desired_acceleration_forest  # noqa: E402
+    fdes, xs = [], []
+    for i in range(400):
+        if i % 10 == 0:
+            acc, _, _ = _desired_acceleration_forest(dyn.state, i * 1e-3, env)
+            f_des, _ = hl.control(dyn.state, acc)
+            fdes.append(f_des.copy())
+        dyn.integrate(ll.control(dyn.state, f_des))
+        s = dyn.state
+        xs.append(np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl]))
+    np.savez(os.path.join(OUT, "ref_closed_loop_sm.npz"), f_des=np.array(fdes), states=np.array(xs))
 
 
 def gen_forest():
@@ -347,13 +375,16 @@ def gen_long_closed_loop(name, T=None, state_every=10):
 if __name__ == "__main__":
     import time
 
+    if len(sys.argv) > 1 and sys.argv[1] == "sm":
+        gen_lowlevel_sm()
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[1] == "long":
         t = time.time()
         gen_long_closed_loop(sys.argv[2])
         print(f"gen_long_closed_loop({sys.argv[2]}): {time.time() - t:.1f}s", flush=True)
         sys.exit(0)
     for fn in (gen_params, gen_dynamics, gen_lowlevel, gen_forest, gen_env_rows, gen_qp, gen_outer_loops,
-               gen_closed_loop):
+               gen_closed_loop, gen_lowlevel_sm):
         t = time.time()
         fn()
         print(f"{fn.__name__}: {time.time() - t:.1f}s", flush=True)

@@ -76,8 +76,16 @@ def env_rows(prm, n, st, trees, agent, alpha):
     return lhs[:k], rhs[:k], bool(col.value), md.value
 
 
-def sim_step(prm, n, st, counter, fdes, dt):
+def sim_step(prm, n, st, counter, fdes, dt, kind=0):
     st = np.array(st, dtype=np.float64)
     c = ctypes.c_int(counter)
-    lib().hs_sim_step(p(prm), n, st.ctypes.data_as(D), ctypes.byref(c), p(fdes), ctypes.c_double(dt))
+    lib().hs_sim_step_ll(p(prm), n, st.ctypes.data_as(D), ctypes.byref(c), p(fdes), ctypes.c_double(dt), int(kind))
     return st, c.value
+
+
+def ll_control(R, w, J, fdes, kind=0):
+    """one agent's low-level law (ll_control_agent): R, J row-major 3x3 (9), w, fdes (3)"""
+    f = ctypes.c_double()
+    M = np.zeros(3)
+    lib().hs_ll_control_kind(p(R), p(w), p(J), p(fdes), ctypes.byref(f), M.ctypes.data_as(D), int(kind))
+    return f.value, M

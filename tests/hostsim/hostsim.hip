@@ -138,8 +138,17 @@ void hs_sim_step(const double* prm, int n, double* st, int* counter, const doubl
   sim_step<16>(prm, n, st, counter, fdes, dt);
 }
 
+void hs_sim_step_ll(const double* prm, int n, double* st, int* counter, const double* fdes, double dt, int kind) {
+  sim_step<16>(prm, n, st, counter, fdes, dt, kind);
+}
+
 void hs_ll_control(const double* R, const double* w, const double* J, const double* fdes, double* f, double* M) {
   ll_control_agent(R, w, J, fdes, f, M);
+}
+
+void hs_ll_control_kind(const double* R, const double* w, const double* J, const double* fdes, double* f, double* M,
+                        int kind) {
+  ll_control_agent(R, w, J, fdes, f, M, kind);
 }
 
 void hs_desired_accel(const double* st, int n, const double* mountain, double x_offset, double* acc) {

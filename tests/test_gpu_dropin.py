@@ -180,3 +180,46 @@ def test_gpu_dropin_controller_closed_loop(tag, name):
         x, _ = sim.get_state()
         ref = system.pack_state(unpack_flat(d[f"{tag}_states"][10 * k + 9], 3))
         assert np.max(np.abs(x[0] - ref)) < 1e-4, k
+
+
+@pytest.mark.parametrize("kind,name", [("pd", "ref_lowlevel.npz"), ("sm", "ref_lowlevel_sm.npz")])
+def test_gpu_low_level_controller_golden(kind, name):
+    """RQPLowLevelController(kind).control (control/rqp_centralized.py:518-535) through k_low_level,
+    batched (dat_low_level_control) and through the single-scenario drop-in, vs the reference."""
+    from distributed_aerial_transportation_amd import BatchedController, RQPLowLevelController, scenarios, system
+
+    d = load(name)
+    K = d["f"].shape[0]
+    p, col, _ = scenarios.rqp_setup(3)
+    eng = BatchedController("cadmm", 3, K, system.pack_params(p, col))
+    eng.set_state(np.stack([_pack(state_from(d, "s_", k)) for k in range(K)]))
+    eng.set_low_level(kind)
+    f, M = eng.low_level(d["f_des"])
+    np.testing.assert_allclose(f, d["f"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(M, d["M"], rtol=1e-10, atol=1e-12)
+    ll = RQPLowLevelController(kind, p, np.pi / 6)
+    for k in range(3):
+        f1, M1 = ll.control(system.RQPState.unpack(_pack(state_from(d, "s_", k)), 3), d["f_des"][k])
+        np.testing.assert_allclose(f1, d["f"][k], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(M1, d["M"][k], rtol=1e-10, atol=1e-12)
+    with pytest.raises(NotImplementedError):
+        RQPLowLevelController("lqr", p, np.pi / 6)
+
+
+def test_gpu_sm_closed_loop_golden():
+    """400 ms of the reference loop with the "sm" law (centralized HL, forest seed 0) fully on device."""
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios, system
+
+    d = load("ref_closed_loop_sm.npz")
+    p, col, s0 = scenarios.rqp_setup(3)
+    eng = BatchedController("centralized", 3, 1, system.pack_params(p, col))
+    eng.set_forests([Forest.seeded(0)])
+    eng.set_low_level("sm")
+    eng.set_state(system.pack_state(s0)[None], np.zeros(1, dtype=np.int32))
+    for k in range(d["f_des"].shape[0]):
+        r = eng.control(None, None)
+        assert _rel(r.f_des[0], d["f_des"][k]) < REL, k
+        eng.rollout(10)
+        x, _ = eng.get_state()
+        ref = system.pack_state(unpack_flat(d["states"][10 * k + 9], 3))
+        assert np.max(np.abs(x[0] - ref)) < 1e-4, k

@@ -142,3 +142,36 @@ def test_rollout_matches_oracle_dynamics():
         for a in ("R", "w", "xl", "vl", "Rl", "wl"):
             np.testing.assert_allclose(getattr(s1, a), getattr(so, a), atol=1e-12)
         assert cnt == so.counter
+
+
+@pytest.mark.parametrize("kind,name", [(0, "ref_lowlevel.npz"), (1, "ref_lowlevel_sm.npz")])
+def test_low_level_law_matches_reference_fixture(kind, name):
+    """ll_control_agent ("pd" / "sm", incl. the swapped T(e_R, r) of utils/so3_tracking_controllers.py:92)
+    against RQPLowLevelController.control of the reference (control/rqp_centralized.py:518-535)."""
+    d = load(name)
+    p = osc.params(3)
+    for k in range(d["f"].shape[0]):
+        for i in range(3):
+            R = d["s_R"][k][:, :, i]
+            f, M = hs.ll_control(R.reshape(-1), d["s_w"][k][:, i], p.J[:, :, i].reshape(-1), d["f_des"][k][:, i], kind)
+            assert f == pytest.approx(d["f"][k][i], rel=1e-13, abs=1e-13)
+            np.testing.assert_allclose(M, d["M"][k][:, i], rtol=1e-11, atol=1e-13)
+
+
+def test_sm_closed_loop_matches_reference():
+    """400 ms of the reference loop with the "sm" law (centralized HL from the fixture's f_des):
+    the host build of sim_step tracks the reference's states within 1e-9."""
+    from distributed_aerial_transportation_amd.system import pack_state
+
+    from tests._golden import unpack_flat
+
+    d = load("ref_closed_loop_sm.npz")
+    prm = _prm(3)
+    p, _, s0 = __import__("distributed_aerial_transportation_amd").scenarios.rqp_setup(3)
+    x, cnt = pack_state(s0), 0
+    for i in range(d["states"].shape[0]):
+        fd = d["f_des"][i // 10]
+        x, cnt = hs.sim_step(prm, 3, x, cnt, fd.T.reshape(-1), 1e-3, kind=1)
+        if i % 50 == 49:
+            ref = pack_state(unpack_flat(d["states"][i], 3))
+            assert np.max(np.abs(x - ref)) < 1e-9, i

@@ -59,12 +59,15 @@ def test_integrate_golden(tag, n):
         np.testing.assert_allclose(getattr(s, a), getattr(s1, a), rtol=1e-12, atol=1e-12)
 
 
-def test_lowlevel_golden():
-    d = load("ref_lowlevel.npz")
+@pytest.mark.parametrize("kind,name", [("pd", "ref_lowlevel.npz"), ("sm", "ref_lowlevel_sm.npz")])
+def test_lowlevel_golden(kind, name):
+    """RQPLowLevelController("pd" / "sm").control (control/rqp_centralized.py:518-535); "sm" includes the
+    swapped T(e_R, r) call of utils/so3_tracking_controllers.py:92."""
+    d = load(name)
     p = osc.params(3)
     for k in range(d["f"].shape[0]):
         s = state_from(d, "s_", k)
-        f, M = om.low_level_control(p, s, d["f_des"][k])
+        f, M = om.low_level_control(p, s, d["f_des"][k], kind)
         np.testing.assert_allclose(f, d["f"][k], rtol=1e-13, atol=1e-13)
         np.testing.assert_allclose(M, d["M"][k], rtol=1e-12, atol=1e-13)
 
