@@ -34,6 +34,10 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md
 # counts IPM iterations and IPM iterations x active rows on device (dat_get_counters).
 FLOPS_FIXED = 7267.0
 FLOPS_PER_ROW = 283.0
+# DD agent QP (MODE_DD: no K_{-i} products, Cholesky of M alone, DD core solve):
+# F_it,DD(R) = 4042 + 283 R per IPM iteration (k_dd; the dual ascent's 2 (6n)^2 per scenario and DD
+# iteration, ~1 % of k_dd's work at C3, is not counted).
+FLOPS_FIXED_DD = 4042.0
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -451,6 +455,7 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     barrier()
     elapsed = t1 - t0
     w = eng.work()
+    kms = eng.kernel_ms()  # k_cadmm / k_dd of the timed steps (before the metrics-only step below)
     res = eng.control(None, L.f64(accs[0]))  # metrics only (outside the timed region)
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
     tot = np.array([w["qp_solves"], w["ipm_iters"], w["hl_kernel_ms"], elapsed, w["ipm_row_iters"]])
@@ -464,9 +469,11 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         if dist is not None:
             dist.destroy_process_group()
         return
-    kernel = {"cadmm": "k_cadmm", "dd": "k_dd_setup+k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
-    launch_ms = float(tot[2]) / max(w["hl_steps"], 1)
-    flops_launch = (FLOPS_FIXED * float(tot[1]) + FLOPS_PER_ROW * float(tot[4])) / max(w["hl_steps"], 1)
+    kernel = {"cadmm": "k_cadmm", "dd": "k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
+    step_ms = float(tot[2]) / max(w["hl_steps"], 1)
+    launch_ms = kms / max(w["hl_steps"], 1) if args.mode != "centralized" else step_ms
+    fixed = FLOPS_FIXED_DD if args.mode == "dd" else FLOPS_FIXED
+    flops_launch = (fixed * float(tot[1]) + FLOPS_PER_ROW * float(tot[4])) / max(w["hl_steps"], 1)
     tflops = flops_launch / max(launch_ms * 1e-3, 1e-12) / 1e12
     work_mode = "fixed work: tol 0, 25 ADMM iterations" if args.fixed_work else "reference loop: tol 1e-2, max_iter 100"
     workload = f"{cfg}: {args.mode} n={n}, QP-level, no env ({work_mode}), {B} scenarios per GPU"
@@ -481,11 +488,12 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
                   "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
-                  "kernel_ms_per_step": launch_ms},
+                  "kernel_ms_per_step": step_ms},
         "roofline": {"bound": "fp64-valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kernel, "launch_ms": launch_ms,
-                     "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"
-                                   + (" (C-ADMM lane count, approximate for DD)" if args.mode == "dd" else "")},
+                     "flops_per_launch": flops_launch,
+                     "flop_model": f"{fixed:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"
+                                   + (" (DD agent QP; dual ascent not counted)" if args.mode == "dd" else "")},
     }
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline_qp(cfg, n, args.mode, args.cpu_sample_s, args.fixed_work)

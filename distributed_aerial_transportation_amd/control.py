@@ -127,7 +127,7 @@ class BatchedController:
         self.cfg.max_iter = max_iter
 
     def set_persistent_blocks(self, blocks: int) -> None:
-        """C-ADMM: resident k_cadmm workgroups draining the scenario queues (0: default)."""
+        """C-ADMM / DD: resident k_cadmm / k_dd workgroups draining the scenario queues (0: default)."""
         L.check(self._lib.dat_set_persistent_blocks(self._h, int(blocks)))
 
     def reset_warm_start(self) -> None:
@@ -259,6 +259,12 @@ class BatchedController:
         L.check(self._lib.dat_get_class_occupancy(self._h, int(env_class), ctypes.byref(sl), ctypes.byref(wp)))
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "kernel_ms": ms.value,
                 "slot_ipm_iters": sl.value, "wave_admm_iters": wp.value}
+
+    def kernel_ms(self) -> float:
+        """Summed device time of k_cadmm / k_dd since the last counter reset (dat_get_kernel_ms)."""
+        ms = ctypes.c_double()
+        L.check(self._lib.dat_get_kernel_ms(self._h, ctypes.byref(ms)))
+        return ms.value
 
     def reset_counters(self) -> None:
         L.check(self._lib.dat_reset_counters(self._h))

@@ -724,14 +724,27 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
 // DD step
 // ------------------------------------------------------------------------------------------------
 constexpr int DD_ES = 7, DD_RS = 5;
+// k_dd_key: drain-order key of every scenario (previous step's DD iteration count, longest first),
+// sorted by k_bucket into one queue (class 0).
+__global__ void k_dd_key(KArgs a) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc < a.B) a.need[sc] = NIB - 1 - iter_bin(a.iters[sc]);
+}
+
+// DD control step (control/rqp_dd.py:695-752), persistent: each 64-lane block holds G = floor(64/n)
+// scenario slots of n lanes (one lane per agent QP) and drains the sorted scenario queue; a slot whose
+// scenario stops is refilled at the next dual-ascent pass.  A scenario's arithmetic does not depend
+// on the slot or block that runs it.  ENV = false (no forest on the handle): every QP has the three
+// base rows only, and the IPM is instantiated for them alone (the register footprint of the 13-slot
+// instantiation is not paid).
+template <bool ENV>
 __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n, N6 = 6 * n;
   const int G = 64 / n, NT = G * n;
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
-  const int sc = blockIdx.x * G + ls;
-  const bool valid = (lane < NT) && (sc < a.B);
+  const int lsc = ls < G ? ls : 0;
   double* X = smem;                 // NT x 9   (f_i, F_i, M_i)
   double* lamF = X + NT * 9;        // G x 3n
   double* lamM = lamF + G * N3;     // G x 3n
@@ -740,58 +753,76 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* red = Rts + G * 9 * n;    // 64 x DD_RS
   QPShared* shs = (QPShared*)(red + 64 * DD_RS);  // G
   double* envs = (double*)(shs + G);              // EnvLds image
-  QPShared& S = shs[ls < G ? ls : 0];
+  int* sid = (int*)(envs + ENV_LDS_DOUBLES);      // G: scenario of the slot (-1 empty, -2 retired)
+  int* done = sid + 64;                           // G: the slot's scenario stopped in this pass
+  QPShared& S = shs[lsc];
   double* myX = X + lane * 9;
-  double* lF = lamF + ls * N3;
-  double* lM = lamM + ls * N3;
-  double* rts = Rts + ls * 9 * n;
+  double* lF = lamF + lsc * N3;
+  double* lM = lamM + lsc * N3;
+  double* rts = Rts + lsc * 9 * n;
+  const int cnt = a.scount[0], first = a.scount[NCLS];
+  const LdsRef<QPShared> shr{shs, lsc};
+  const EnvLds err{envs, lane};
+  const RtLds rtr{Rts, lsc * 9 * n + 9 * i};
+  if (lane < G) sid[lane] = -1;
+  __syncthreads();
 
   QPLane<1> P;
   const double* prm = nullptr;
+  const double* Rl = nullptr;
+  double* bst = nullptr;
   double prev[9];
-  int iter = 0, qstat = ST_OPTIMAL;
+  int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
+  double mdist = 0.0;
   long long my_ipm = 0, my_qp = 0, my_rowit = 0;
-  EnvOut env;
-  env.collision = 0;
-  env.min_env_dist = 0.0;
-  if (valid) {
-    prm = prm_of(a, sc);
-    const double* st = a.state + (size_t)sc * a.S;
-    make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + 9 * i);
-    for (int c = 0; c < 3; ++c) {
-      lF[3 * i + c] = a.dlamF[(size_t)sc * N3 + 3 * i + c];
-      lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
-    }
-    for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
-    for (int c = 0; c < 9; ++c) myX[c] = prev[c];  // the controller's current (f, F, M)
-    if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
-  }
-  if (lane < 64) red[lane * DD_RS + 3] = valid ? 0.0 : 1.0;  // stop flag per lane group leader
-  __syncthreads();
-  int nr = NBASE;
-  if (valid) {
-    const double* st = a.state + (size_t)sc * a.S;
-    lane_dd_static(P, prm, i);
-    const double* trees;
-    int nt;
-    unsigned emask;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
-    EnvRows Ev;
-    set_env_rows(P, Ev, S, emask, lhs, rhs);
-    env_to_lds(envs, lane, Ev);
-    nr = rows_needed(P.emask);
-  }
-  nr = wave_max(nr);
-  const LdsRef<QPShared> shr{shs, ls < G ? ls : 0};
-  const EnvLds err{envs, lane};
-  const RtLds rtr{Rts, (ls < G ? ls : 0) * 9 * n + 9 * i};
-  double* bst = a.best + (valid ? ((size_t)sc * n + i) * best_size(1) : 0);
-  const double* y0 = valid ? prm + DAT_P_FEQ(n) + 3 * i : nullptr;
-  const double* Rl = valid ? a.state + (size_t)sc * a.S + DAT_S_RL(n) : nullptr;
   for (;;) {
-    const bool active = valid && red[(ls * n) * DD_RS + 3] == 0.0;
+    // ---- refill empty slots from the queue
+    if (lane < NT && i == 0 && sid[ls] == -1) {
+      const int q = atomicAdd(a.qhead, 1);
+      sid[ls] = q < cnt ? a.slist[first + q] : -2;
+      done[ls] = 0;
+    }
+    __syncthreads();
+    const int slot_sc = lane < NT ? sid[ls] : -2;
+    const bool fresh = slot_sc >= 0 && slot_sc != sc;
+    if (fresh) {
+      sc = slot_sc;
+      prm = prm_of(a, sc);
+      const double* st = a.state + (size_t)sc * a.S;
+      Rl = st + DAT_S_RL(n);
+      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, Rl, rts + 9 * i);
+      for (int c = 0; c < 3; ++c) {
+        lF[3 * i + c] = a.dlamF[(size_t)sc * N3 + 3 * i + c];
+        lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
+      }
+      for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
+      for (int c = 0; c < 9; ++c) myX[c] = prev[c];  // the controller's current (f, F, M)
+      bst = a.best + ((size_t)sc * n + i) * best_size(1);
+      iter = 0;
+      qstat = ST_OPTIMAL;
+      if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
+    }
+    if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
+    if (fresh) {
+      lane_dd_static(P, prm, i);
+      col = 0;
+      mdist = prm[DAT_P_VISR];
+      if (ENV) {
+        const double* trees;
+        int nt;
+        unsigned emask;
+        forest_of(a, sc, &trees, &nt);
+        double lhs[DAT_NENV][3], rhs[DAT_NENV];
+        EnvOut env = env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
+        col = env.collision;
+        mdist = env.min_env_dist;
+        EnvRows Ev;
+        set_env_rows(P, Ev, S, emask, lhs, rhs);
+        env_to_lds(envs, lane, Ev);
+      }
+    }
+    const bool active = slot_sc >= 0;
+    const int nr = wave_max(active ? rows_needed(P.emask) : NBASE);
     if (active) {
       // prices (control/rqp_dd.py:718-722)
       double sF[3] = {0, 0, 0}, sM[3] = {0, 0, 0};
@@ -808,7 +839,10 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       }
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, IPM_TOL);
+      IPMOut o = ENV ? ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
+                                                  IPM_MAX_ITER, IPM_TOL)
+                     : ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                                    IPM_TOL);
       my_ipm += o.iters;
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
@@ -829,6 +863,9 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         mv3(prm + DAT_P_JTI, rf, jr);
         for (int c = 0; c < 3; ++c) prev[6 + c] = -jr[c];
       }
+    }
+    __syncthreads();  // agent 0's fallback above reads X before this pass's writes
+    if (active) {
       for (int c = 0; c < 9; ++c) myX[c] = prev[c];
     }
     __syncthreads();
@@ -847,6 +884,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         E[lane * DD_ES + c] = myX[3 + c] - sf[c];
         E[lane * DD_ES + 3 + c] = myX[6 + c] - sm[c];
       }
+      red[lane * DD_RS + 0] = col ? 1.0 : 0.0;
+      red[lane * DD_RS + 1] = mdist;
     }
     __syncthreads();
     if (active && i == 0) {
@@ -856,58 +895,50 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int k = 0; k < n; ++k) s += fabs(E[(ls * n + k) * DD_ES + r]);
         res = fmax(res, s);
       }
-      bool stop = (res < a.res_tol) || (iter > a.max_iter);
+      const bool stop = (res < a.res_tol) || (iter > a.max_iter);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
-      red[(ls * n) * DD_RS + 2] = stop ? 1.0 : 0.0;
+      done[ls] = stop ? 1 : 0;
     }
     __syncthreads();
-    if (active && red[(ls * n) * DD_RS + 2] == 0.0) {
-      // dual ascent: lambda += H^-1 (A x)   (control/rqp_dd.py:678-693); rows 6i..6i+5
-      const double* Hi = a.dHinv + (size_t)sc * N6 * N6;
-      double stp[6];
-      for (int r = 0; r < 6; ++r) {
-        const double* row = Hi + (size_t)(6 * i + r) * N6;
-        double s = 0.0;
-        for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * DD_ES + c % 6];
-        stp[r] = s;
-      }
-      red[lane * DD_RS + 0] = 0.0;
-      for (int c = 0; c < 3; ++c) {
-        lF[3 * i + c] += stp[c];
-        lM[3 * i + c] += stp[3 + c];
+    if (active) {
+      if (!done[ls]) {
+        // dual ascent: lambda += H^-1 (A x)   (control/rqp_dd.py:678-693); rows 6i..6i+5
+        const double* Hi = a.dHinv + (size_t)sc * N6 * N6;
+        double stp[6];
+        for (int r = 0; r < 6; ++r) {
+          const double* row = Hi + (size_t)(6 * i + r) * N6;
+          double s = 0.0;
+          for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * DD_ES + c % 6];
+          stp[r] = s;
+        }
+        for (int c = 0; c < 3; ++c) {
+          lF[3 * i + c] += stp[c];
+          lM[3 * i + c] += stp[3 + c];
+        }
+      } else {
+        // the scenario stopped: write its outputs and free the slot
+        for (int c = 0; c < 3; ++c) {
+          a.dlamF[(size_t)sc * N3 + 3 * i + c] = lF[3 * i + c];
+          a.dlamM[(size_t)sc * N3 + 3 * i + c] = lM[3 * i + c];
+          a.fdes[(size_t)sc * N3 + 3 * i + c] = myX[c];
+        }
+        for (int c = 0; c < 9; ++c) a.dprev[((size_t)sc * n + i) * 9 + c] = prev[c];
+        a.qstatus[(size_t)sc * n + i] = qstat;
+        if (i == 0) {
+          a.iters[sc] = iter;
+          int coll = 0;
+          double md = prm[DAT_P_VISR];
+          for (int k = 0; k < n; ++k) {
+            coll |= red[(ls * n + k) * DD_RS] != 0.0;
+            md = fmin(md, red[(ls * n + k) * DD_RS + 1]);
+          }
+          a.col[sc] = (unsigned char)coll;
+          a.mind[sc] = md;
+          sid[ls] = -1;
+        }
       }
     }
     __syncthreads();
-    int any = 0;
-    if (active && i == 0) {
-      bool stop = red[(ls * n) * DD_RS + 2] != 0.0;
-      red[(ls * n) * DD_RS + 3] = stop ? 1.0 : 0.0;
-      any = stop ? 0 : 1;
-    }
-    if (!__syncthreads_or(any)) break;
-  }
-  if (valid) {
-    for (int c = 0; c < 3; ++c) {
-      a.dlamF[(size_t)sc * N3 + 3 * i + c] = lF[3 * i + c];
-      a.dlamM[(size_t)sc * N3 + 3 * i + c] = lM[3 * i + c];
-      a.fdes[(size_t)sc * N3 + 3 * i + c] = myX[c];
-    }
-    for (int c = 0; c < 9; ++c) a.dprev[((size_t)sc * n + i) * 9 + c] = prev[c];
-    a.qstatus[(size_t)sc * n + i] = qstat;
-    red[lane * DD_RS + 0] = env.collision ? 1.0 : 0.0;
-    red[lane * DD_RS + 1] = env.min_env_dist;
-  }
-  __syncthreads();
-  if (valid && i == 0) {
-    a.iters[sc] = iter;
-    int coll = 0;
-    double md = prm[DAT_P_VISR];
-    for (int k = 0; k < n; ++k) {
-      coll |= red[(ls * n + k) * DD_RS] != 0.0;
-      md = fmin(md, red[(ls * n + k) * DD_RS + 1]);
-    }
-    a.col[sc] = (unsigned char)coll;
-    a.mind[sc] = md;
   }
   unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
   for (int off = 32; off > 0; off >>= 1) {
@@ -1309,7 +1340,7 @@ KArgs kargs(dat_handle* h) {
 size_t dd_lds(int n) {
   int G = 64 / n, NT = G * n;
   return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * DD_ES + (size_t)G * 9 * n + 64 * DD_RS) +
-         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES;
+         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES + sizeof(int) * 128;
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
@@ -1333,9 +1364,15 @@ int launch_hl(dat_handle* h) {
                        h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
+    hipLaunchKernelGGL(k_dd_key, dim3((B + 63) / 64), dim3(64), 0, h->stream, a);
+    hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
+    HIPCHK(hipEventRecord(h->ek, h->stream));
     int G = 64 / n;
     int blocks = (B + G - 1) / G;
-    hipLaunchKernelGGL(k_dd, dim3(blocks), dim3(64), dd_lds(n), h->stream, a);
+    if (h->nforest > 0)
+      hipLaunchKernelGGL(k_dd<true>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n), h->stream, a);
+    else
+      hipLaunchKernelGGL(k_dd<false>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n), h->stream, a);
   } else {
     int blocks = (B + 63) / 64;
     if (n == 3)
@@ -1353,7 +1390,7 @@ int finish_hl(dat_handle* h) {
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, h->e0, h->e1));
   h->hl_ms += ms;
-  if (h->cfg.mode == DAT_MODE_CADMM) {
+  if (h->cfg.mode != DAT_MODE_CENTRALIZED) {  // k_cadmm / k_dd: from after k_bucket to the end of the step
     float mk = 0.f;
     HIPCHK(hipEventElapsedTime(&mk, h->ek, h->e1));
     h->cadmm_ms += mk;
@@ -1440,6 +1477,9 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
   } else if (c.mode == DAT_MODE_DD) {
+    rc |= dalloc(h, &h->need, B);
+    rc |= dalloc(h, &h->slist, B);
+    rc |= dalloc(h, &h->scount, 3 * NCLS);
     rc |= dalloc(h, &h->dlamF, B * N3);
     rc |= dalloc(h, &h->dlamM, B * N3);
     rc |= dalloc(h, &h->dprev, B * n * 9);
@@ -1861,6 +1901,12 @@ int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, do
   (void)hipFree(df);
   (void)hipFree(dm);
   if (e != hipSuccess) return fail(std::string("dat_low_level_control: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int dat_get_kernel_ms(dat_handle* h, double* ms) {
+  if (!h || !ms) return fail("dat_get_kernel_ms: null argument");
+  *ms = h->cadmm_ms;
   return 0;
 }
 

@@ -139,10 +139,14 @@ int dat_get_class_counters(dat_handle* h, int env_class, long long* qp_solves, l
 int dat_get_class_occupancy(dat_handle* h, int env_class, long long* slot_ipm_iters, long long* wave_admm_iters);
 int dat_reset_counters(dat_handle* h);
 int dat_synchronize(dat_handle* h);
-/* C-ADMM: number of resident k_cadmm workgroups that drain the scenario queues (0 = default,
+/* C-ADMM / DD: number of resident k_cadmm / k_dd workgroups that drain the scenario queues (0 = default,
  * 4 x CUs).  A scenario's arithmetic does not depend on it; tests cap it at 1-2 workgroups so that
  * scenario slots are refilled many times within one control step. */
 int dat_set_persistent_blocks(dat_handle* h, int blocks);
+/* Summed device time [ms] since the last counter reset of the main solver kernel of each control step:
+ * k_cadmm (C-ADMM) or k_dd (DD; the per-scenario quasi-Newton setup k_dd_setup excluded), 0 for
+ * centralized.  Both are persistent queue drains; dat_set_persistent_blocks caps their grid. */
+int dat_get_kernel_ms(dat_handle* h, double* ms);
 
 /* ---- raw batched kernels (tests / benchmarking of single pieces) ---------------------------
  * dat_env_rows: _set_collision_avoidance_cbf_parameters (control/rqp_cadmm.py:307-373,

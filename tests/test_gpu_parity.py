@@ -325,3 +325,36 @@ def test_gpu_failure_branches(mode):
     if mode == "cadmm":
         feq = om.equilibrium_forces(osc.params(n))
         assert _rel(r1.f_des[2], feq) < 1e-12
+
+
+def test_gpu_dd_persistent_drain():
+    """k_dd drains a sorted scenario queue with slot refill: B = 48 scenarios (n = 6, G = 10 slots per
+    workgroup) on a grid capped at 2 workgroups, two consecutive steps (warm multipliers), must give
+    exactly the results of the uncapped grid (a scenario's arithmetic does not depend on its slot),
+    every agent QP OPTIMAL, and a sample must match the oracle (iterations exact, f_des within 1e-5)."""
+    from distributed_aerial_transportation_amd import scenarios
+
+    n, B = 6, 48
+    rng = np.random.default_rng(606)
+    states = scenarios.perturbed_states(n, B, rng)
+    a1 = rng.uniform(-0.5, 0.5, (B, 6)) * 6.0
+    a2 = rng.uniform(-0.5, 0.5, (B, 6)) * 6.0
+    runs = []
+    for blocks in (2, 0):
+        eng = _eng("dd", n, B, record_err=True)
+        eng.set_persistent_blocks(blocks)
+        runs.append((eng.control(states, a1), eng.control(states, a2)))
+    for r_cap, r_full in zip(*runs):
+        np.testing.assert_array_equal(r_cap.f_des, r_full.f_des)
+        np.testing.assert_array_equal(r_cap.iters, r_full.iters)
+        assert np.all(r_cap.qp_status == 0)
+    r1, r2 = runs[0]
+    for b in range(0, B, 8):
+        ctl = oc.DD(osc.params(n), osc.col_radius(n))
+        s = _ostate(states[b], n)
+        f1, st1 = ctl.control(s, (a1[b, :3], a1[b, 3:]))
+        f2, st2 = ctl.control(s, (a2[b, :3], a2[b, 3:]))
+        if _ambiguous(st1.err_seq) or _ambiguous(st2.err_seq):
+            continue
+        assert r1.iters[b] == st1.iter and r2.iters[b] == st2.iter, (b, r1.iters[b], st1.iter, r2.iters[b], st2.iter)
+        assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL
