@@ -8,6 +8,7 @@ hand-written fp64 HIP kernels for gfx950 behind the C-ABI in include/dat.h.
 from . import layout, scenarios, system  # noqa: F401  (host-side data, no GPU needed)
 from .env_forest import Forest  # noqa: F401
 from .system import RQPCollision, RQPParameters, RQPState, pack_params, pack_state  # noqa: F401
+from . import rigid_payload  # noqa: F401  (RPCentralizedController / RPDynamics load libdat.so on use)
 
 
 def __getattr__(name):

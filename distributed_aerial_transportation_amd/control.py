@@ -190,6 +190,13 @@ class BatchedController:
             fd = L.f64(np.asarray(f_des).transpose(0, 2, 1).reshape(self.batch, 3 * self.n))
         L.check(self._lib.dat_rollout(self._h, int(steps), L.ptr(fd)))
 
+    def rp_rollout(self, steps: int, f: Optional[np.ndarray] = None) -> None:
+        """Rigid-payload dynamics (dat_rp_rollout) with forces f (B, 3, n) held for `steps` steps."""
+        fd = None
+        if f is not None:
+            fd = L.f64(np.asarray(f).transpose(0, 2, 1).reshape(self.batch, 3 * self.n))
+        L.check(self._lib.dat_rp_rollout(self._h, int(steps), L.ptr(fd)))
+
     def closed_loop(self, hl_steps: int) -> None:
         L.check(self._lib.dat_closed_loop(self._h, int(hl_steps)))
 

@@ -1061,6 +1061,18 @@ __global__ void k_low_level(KArgs a, const double* fdes, double* fo, double* Mo)
                    fdes + (size_t)sc * 3 * n + 3 * i, fo + t, Mo + 3 * (size_t)t, a.ll_kind);
 }
 
+// rigid payload (system/rigid_payload.py:93-130): `steps` steps of dt with the forces f held, one lane per scenario
+__global__ void k_rp_rollout(KArgs a, int steps, double dt, const double* f) {
+  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sc >= a.B) return;
+  const int n = a.n;
+  const double* prm = prm_of(a, sc);
+  double* st = a.state + (size_t)sc * a.S;
+  int cnt = a.counter[sc];
+  for (int s = 0; s < steps; ++s) rp_step(prm, n, st, &cnt, f + (size_t)sc * 3 * n, dt);
+  a.counter[sc] = cnt;
+}
+
 __global__ void k_desired(KArgs a, double* acc) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
   if (sc >= a.B) return;
@@ -1907,6 +1919,21 @@ int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, do
 int dat_get_kernel_ms(dat_handle* h, double* ms) {
   if (!h || !ms) return fail("dat_get_kernel_ms: null argument");
   *ms = h->cadmm_ms;
+  return 0;
+}
+
+int dat_rp_rollout(dat_handle* h, int steps, const double* f) {
+  if (!h) return fail("null handle");
+  if (steps <= 0) return 0;
+  if (!h->have_params) return fail("dat_rp_rollout: params not set");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n;
+  if (f) HIPCHK(hipMemcpyAsync(h->fdes, f, sizeof(double) * B * 3 * n, hipMemcpyHostToDevice, h->stream));
+  KArgs a = kargs(h);
+  hipLaunchKernelGGL(k_rp_rollout, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, steps, h->cfg.dt,
+                     (const double*)h->fdes);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
 

@@ -712,6 +712,49 @@ DAT_HD void sim_step(const double* prm, int n, double* st, int* counter, const d
   }
 }
 
+// One step of the rigid payload driven by actuator forces f (3n, agent-major, ground frame) --
+// RPDynamics.forward_dynamics + RPState.integrate (system/rigid_payload.py:76-90, 109-130), on the
+// payload part of a dat state block with the rigid-payload parameter block (mT = ml, JT = Jl,
+// r_com = r): ml dvl = sum f - ml g e3, Jl dwl + wl x Jl wl = sum hat(r_i) Rl' f_i.
+DAT_HD void rp_step(const double* prm, int n, double* st, int* counter, const double* f, double dt) {
+  double* xl = st + DAT_S_XL(n);
+  double* vl = st + DAT_S_VL(n);
+  double* Rl = st + DAT_S_RL(n);
+  double* wl = st + DAT_S_WL(n);
+  const double ml = prm[DAT_P_MT];
+  const double* Jl = prm + DAT_P_JT;
+  const double* Jli = prm + DAT_P_JTI;
+  const double* r = prm + DAT_P_RCOM(n);
+  double F[3] = {0, 0, 0}, Mo[3] = {0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    double fb[3], m3[3];
+    mtv3(Rl, f + 3 * i, fb);
+    cross3(r + 3 * i, fb, m3);
+    for (int c = 0; c < 3; ++c) { F[c] += f[3 * i + c]; Mo[c] += m3[c]; }
+  }
+  double dvl[3] = {F[0] / ml, F[1] / ml, F[2] / ml - DAT_GRAVITY};
+  double Jw[3], wJw[3], t[3], dwl[3];
+  mv3(Jl, wl, Jw);
+  cross3(wl, Jw, wJw);
+  for (int c = 0; c < 3; ++c) t[c] = Mo[c] - wJw[c];
+  mv3(Jli, t, dwl);
+  for (int c = 0; c < 3; ++c) {
+    xl[c] = xl[c] + vl[c] * dt + dvl[c] * dt * dt / 2.0;
+    vl[c] = vl[c] + dvl[c] * dt;
+  }
+  double v[3], E[9], Rn[9];
+  for (int c = 0; c < 3; ++c) v[c] = (wl[c] + dwl[c] * dt / 2.0) * dt;
+  exp3(v, E);
+  mm3(Rl, E, Rn);
+  for (int c = 0; c < 9; ++c) Rl[c] = Rn[c];
+  for (int c = 0; c < 3; ++c) wl[c] += dwl[c] * dt;
+  *counter += 1;
+  if (*counter >= 20) {  // _INTEGRATION_STEPS_PER_ROTATION_PROJECTION (system/rigid_payload.py:11)
+    polar3(Rl);
+    *counter = 0;
+  }
+}
+
 // _desired_acceleration_forest (example/rqp_example.py:33-59); acc = (dvl_des, dwl_des)
 DAT_HD void desired_accel_forest(const double* st, int n, const double* mountain, double x_offset, double* acc) {
   const double* xl = st + DAT_S_XL(n);

@@ -116,6 +116,12 @@ int dat_set_low_level(dat_handle* h, int kind);
  * current states: f_des B x 3n (agent-major) or NULL (the last control step's output); thrust B x n,
  * moment B x n x 3 (agent-major 3-vectors). */
 int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, double* moment);
+/* Rigid payload driven by actuator forces (RPDynamics.integrate, system/rigid_payload.py:93-172): `steps`
+ * steps of dt on the payload part of the states (xl, vl, Rl, wl; Rl projected every 20 steps), forces
+ * f B x 3n (agent-major, ground frame; NULL: the last control step's output) held.  The handle carries
+ * the rigid-payload parameter block (rigid_payload.pack_rp_params: mT = ml, JT = Jl, r_com = r), whose
+ * centralized QP is RPCentralizedController (control/rp_centralized.py:9-306) via dat_control_step. */
+int dat_rp_rollout(dat_handle* h, int steps, const double* f);
 
 /* ---- device-resident closed loop (the loop of example/rqp_example.py:120-131 with the desired
  * acceleration of :33-59): hl_steps x (desired acceleration + control step +

@@ -23,6 +23,8 @@ What each fixture pins (reference file:line):
   ref_closed_loop.npz rqp_example-style closed loop (HL every 10)   example/rqp_example.py:120-131
   ref_lowlevel_sm.npz RQPLowLevelController("sm").control          utils/so3_tracking_controllers.py:52-95
   ref_closed_loop_sm.npz  400 ms centralized loop with the "sm" law  control/rqp_centralized.py:474-478
+  ref_rp.npz          RPCentralizedController + RPDynamics closed loop control/rp_centralized.py:9-302,
+                      (test/control/test_rpcentralized.py:main, 20 s)  system/rigid_payload.py:93-130
   ref_long_<tag>.npz  rqp_example over the reference horizon (100 s; DD 10 s): f_des, iters, min_dist per HL
                       step, x_err / v_err per log step, states + LL wrench every 10th log step
                       (python -O make_golden.py long <controller_type>)
@@ -328,6 +330,43 @@ def gen_closed_loop(steps=400):
     np.savez(os.path.join(OUT, "ref_closed_loop.npz"), **out)
 
 
+def gen_rp():
+    """RPCentralizedController (control/rp_centralized.py:9-302) and RPDynamics (system/rigid_payload.py:
+    93-130): the closed loop of test/control/test_rpcentralized.py:main (n = 3, dt = 10e-3, circle tracking
+    law :14-37) for 20 s -- f per step and the state after each step -- plus forward-dynamics cases at
+    random states / forces."""
+    sys.path.insert(0, os.path.join(REF, "test", "control"))
+    from control.rp_centralized import RPCentralizedController
+    from example.setup import rp_setup
+    from system.rigid_payload import RPDynamics, RPState
+    from test_rpcentralized import _desired_acceleration
+
+    params, col, s0 = rp_setup(3)
+    dt = 10e-3
+    ctl = RPCentralizedController(params, col, s0, dt)
+    dyn = RPDynamics(params, s0, dt)
+    t_seq = np.arange(0, 20, dt)
+    fs, xs, accs = [], [], []
+    for i in range(len(t_seq)):
+        acc_des, _, _ = _desired_acceleration(dyn.state, t_seq[i])
+        f = ctl.control(dyn.state, acc_des)
+        dyn.integrate(f)
+        s = dyn.state
+        fs.append(np.array(f).copy()), accs.append(np.concatenate(acc_des))
+        xs.append(np.concatenate([s.xl, s.vl, s.Rl.reshape(-1), s.wl]))
+    rng = np.random.default_rng(17)
+    fd_s, fd_f, fd_acc = [], [], []
+    for _ in range(16):
+        s = RPState(rng.uniform(-1, 1, 3), rng.uniform(-1, 1, 3), rand_rot(rng, 0.5), rng.uniform(-1, 1, 3))
+        f = np.vstack([rng.uniform(-1, 1, (2, 3)), rng.uniform(0, 2, (1, 3))])
+        d = RPDynamics(params, s, dt)
+        fd_s.append(np.concatenate([s.xl, s.vl, s.Rl.reshape(-1), s.wl])), fd_f.append(f)
+        fd_acc.append(np.concatenate(d.forward_dynamics(f)))
+    np.savez(os.path.join(OUT, "ref_rp.npz"), ml=params.ml, Jl=params.Jl, r=params.r, f_eq=ctl.f_eq, dt=dt,
+             f=np.array(fs), states=np.array(xs), acc=np.array(accs), min_fz=ctl.min_fz, max_f=ctl.max_f,
+             fd_s=np.array(fd_s), fd_f=np.array(fd_f), fd_acc=np.array(fd_acc))
+
+
 LONG_T = {"centralized": 100.0, "consensus-admm": 100.0, "dual-decomposition": 10.0}
 
 
@@ -375,6 +414,9 @@ def gen_long_closed_loop(name, T=None, state_every=10):
 if __name__ == "__main__":
     import time
 
+    if len(sys.argv) > 1 and sys.argv[1] == "rp":
+        gen_rp()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sm":
         gen_lowlevel_sm()
         sys.exit(0)
@@ -384,7 +426,7 @@ if __name__ == "__main__":
         print(f"gen_long_closed_loop({sys.argv[2]}): {time.time() - t:.1f}s", flush=True)
         sys.exit(0)
     for fn in (gen_params, gen_dynamics, gen_lowlevel, gen_forest, gen_env_rows, gen_qp, gen_outer_loops,
-               gen_closed_loop, gen_lowlevel_sm):
+               gen_closed_loop, gen_lowlevel_sm, gen_rp):
         t = time.time()
         fn()
         print(f"{fn.__name__}: {time.time() - t:.1f}s", flush=True)

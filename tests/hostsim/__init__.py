@@ -89,3 +89,11 @@ def ll_control(R, w, J, fdes, kind=0):
     M = np.zeros(3)
     lib().hs_ll_control_kind(p(R), p(w), p(J), p(fdes), ctypes.byref(f), M.ctypes.data_as(D), int(kind))
     return f.value, M
+
+
+def rp_step(prm, n, st, counter, f, dt):
+    """rigid-payload step (rp_step): f (3n) agent-major"""
+    st = np.array(st, dtype=np.float64)
+    c = ctypes.c_int(counter)
+    lib().hs_rp_step(p(prm), n, st.ctypes.data_as(D), ctypes.byref(c), p(f), ctypes.c_double(dt))
+    return st, c.value

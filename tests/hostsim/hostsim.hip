@@ -142,6 +142,10 @@ void hs_sim_step_ll(const double* prm, int n, double* st, int* counter, const do
   sim_step<16>(prm, n, st, counter, fdes, dt, kind);
 }
 
+void hs_rp_step(const double* prm, int n, double* st, int* counter, const double* f, double dt) {
+  rp_step(prm, n, st, counter, f, dt);
+}
+
 void hs_ll_control(const double* R, const double* w, const double* J, const double* fdes, double* f, double* M) {
   ll_control_agent(R, w, J, fdes, f, M);
 }
