@@ -14,7 +14,7 @@ tools/long_sensitivity.py re-runs the reference's own loop (tests/golden/refstub
 answered by the oracle IPM) with only the QP tolerance changed (1e-11 -> 1e-10 or 1e-12), and the
 centralized loop's f_des leaves 1e-5 at HL step 3054-3055 and its states leave 1e-4 at step 3060
 (t = 30.6 s, a discrete switch of the forest CBF rows).  The GPU run is required to match (f_des 1e-5,
-iteration counts exact, states / x_err / v_err / w 1e-4, min_env_dist 1e-6) up to that
+iteration counts exact, states / x_err / v_err / w / min_env_dist 1e-4) up to that
 reproducibility horizon REPRO_HL (at most the recorded horizon); beyond it both runs are valid closed
 loops of the same controller and the test requires only that the GPU run completes the horizon
 without a collision and with mean tracking errors within 10 % of the reference's.
@@ -80,7 +80,8 @@ def test_gpu_long_closed_loop_logs(tag, ct, capsys):
         np.testing.assert_array_equal(np.array(logs["iter_seq"])[:H], d["iters"][:H])
     else:
         assert logs["iter_seq"] == []
-    np.testing.assert_allclose(logs["min_env_dist_seq"][:H], d["min_dist"][:H], rtol=0, atol=1e-6)
+    # the distance moves with the state: same 1e-4 bound
+    np.testing.assert_allclose(logs["min_env_dist_seq"][:H], d["min_dist"][:H], rtol=0, atol=1e-4)
     np.testing.assert_allclose(logs["x_err_seq"][:Hl], d["x_err"][:Hl], rtol=0, atol=1e-4)
     np.testing.assert_allclose(logs["v_err_seq"][:Hl], d["v_err"][:Hl], rtol=0, atol=1e-4)
     w = np.array([np.concatenate([fw.reshape(-1), Mw.reshape(-1)]) for fw, Mw in logs["w_seq"][::every]])
