@@ -15,4 +15,8 @@ timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc2 -o run --output-format csv -- python3 $ARGS > $OUT/pmc2.log 2>&1 || exit 13
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc3 -o run --output-format csv -- python3 $ARGS > $OUT/pmc3.log 2>&1 || exit 14
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-trace -d $OUT/pmc4 -o run --output-format csv -- python3 $ARGS > $OUT/pmc4.log 2>&1 || exit 15
+# pass 6 (optional): LDS / vector-memory instruction mix (scratch spills are VMEM); names checked against -L
+if grep -q "SQ_INSTS_VMEM_RD" $OUT/counters_list.txt 2>/dev/null; then
+  timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU --kernel-trace -d $OUT/pmc5 -o run --output-format csv -- python3 $ARGS > $OUT/pmc5.log 2>&1 || echo "pass 6 failed"
+fi
 echo done
