@@ -35,6 +35,11 @@ constexpr int NBASE = 3;          // base slots shared by all agents of a scenar
 #define DAT_IPM_NREF 2
 #endif
 constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton solve
+// refinement passes stop early once the linearised system's residual is at rounding level
+// (1 = default; 0: always NREF passes; 2: also none while mu > 1e-3 -- measured no faster)
+#ifndef DAT_IPM_REFINE_MODE
+#define DAT_IPM_REFINE_MODE 1
+#endif
 
 struct QPShared {
   double inv_mT, Bv[9], JTi[9], bv[3], bw[3];
@@ -986,8 +991,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
       rows_adj(zw, bu);
       core(bk, Rf, bu, true, false, dy, dwv, du);
+#if DAT_IPM_REFINE_MODE >= 2
+      const int nref = (gap * ideg > 1e-3) ? 0 : NREF;  // far from the solution: plain Newton directions
+#else
+      const int nref = NREF;
+#endif
 #pragma unroll 1
-      for (int ref = 0; ref < NREF; ++ref) {
+      for (int ref = 0; ref < nref; ++ref) {
         // linearised dual residual of the full system at (dy, dw); refine
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -1033,6 +1043,18 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int r = 0; r < 6; ++r) ef[r] = 0.0;
         }
+#if DAT_IPM_REFINE_MODE >= 1
+        {  // the linearised system is already solved to rounding: the correction would be noise
+          double en = 0.0, sc = 1.0;
+#pragma unroll
+          for (int k = 0; k < NB; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { en = fmax(en, fabs(ek[k][c])); sc = fmax(sc, fabs(rk[k][c])); }
+#pragma unroll
+          for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(Rf[r])); }
+          if (en <= 1e-14 * sc) break;
+        }
+#endif
         core(ek, ef, nullptr, false, true, dy, dwv, du);
       }
 #pragma unroll
