@@ -11,9 +11,10 @@ divergence onset).
 
 The reference loop is not reproducible beyond a finite horizon even against itself:
 tools/long_sensitivity.py re-runs the reference's own loop (tests/golden/refstubs.py, every QP
-answered by the oracle IPM) with only the QP tolerance changed (1e-11 -> 1e-10 or 1e-12), and the
+answered by the oracle IPM) with only the QP tolerance changed (1e-11 -> 1e-10 or 1e-12): the
 centralized loop's f_des leaves 1e-5 at HL step 3054-3055 and its states leave 1e-4 at step 3060
-(t = 30.6 s, a discrete switch of the forest CBF rows).  The GPU run is required to match (f_des 1e-5,
+(t = 30.6 s, a discrete switch of the forest CBF rows); the C-ADMM loop's f_des at step 667 (an
+ADMM iteration count flips at the 1e-2 stopping threshold) and its states at step 2280.  The GPU run is required to match (f_des 1e-5,
 iteration counts exact, states / x_err / v_err / w / min_env_dist 1e-4) up to that
 reproducibility horizon REPRO_HL (at most the recorded horizon); beyond it both runs are valid closed
 loops of the same controller and the test requires only that the GPU run completes the horizon
@@ -34,8 +35,11 @@ pytestmark = pytest.mark.gpu
 # (tools/long_sensitivity.py; None: the whole recorded horizon).  Centralized: states to 3000 (the
 # reference's own split is at 3060); f_des to 2500 -- the GPU run meets a near-switch of the forest
 # rows at step 2543 with its state ~3e-6 away from the reference's and f_des moves by 1.1e-5 there.
-REPRO_HL = {"cent": 3000, "cons": None, "dual": None}
-REPRO_HL_F = {"cent": 2500, "cons": None, "dual": None}
+# C-ADMM: the reference's own loop (QP tol 1e-10 vs 1e-11) keeps f_des within 1e-5 only to HL step
+# 667 (an ADMM iteration count flips at the 1e-2 threshold) and its states within 1e-4 to step 2280;
+# the GPU run holds both to step ~2446 (measured), and is required to within the reference's own.
+REPRO_HL = {"cent": 3000, "cons": 2280, "dual": None}
+REPRO_HL_F = {"cent": 2500, "cons": 667, "dual": None}
 
 
 def _rel(a, b):
@@ -77,7 +81,7 @@ def test_gpu_long_closed_loop_logs(tag, ct, capsys):
     assert np.all(df[:H] < 2e-5)
     assert np.all(ds[: H // every] < 1e-4)
     if ct != "centralized":
-        np.testing.assert_array_equal(np.array(logs["iter_seq"])[:H], d["iters"][:H])
+        np.testing.assert_array_equal(np.array(logs["iter_seq"])[:HF], d["iters"][:HF])
     else:
         assert logs["iter_seq"] == []
     # the distance moves with the state: same 1e-4 bound
