@@ -168,66 +168,6 @@ DAT_HD bool inv3_spd(const double* D, double* O) {
   return true;
 }
 
-// 6x6 LU with partial pivoting, in place, every index compile-time (the row exchange is a
-// predicated swap, so the matrix stays in registers).  piv[k]: row exchanged with k at step k.
-DAT_HD bool lu6(double A[6][6], int piv[6]) {
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    int p = k;
-    double mx = fabs(A[k][k]);
-#pragma unroll
-    for (int r = k + 1; r < 6; ++r) {
-      double v = fabs(A[r][k]);
-      if (v > mx) { mx = v; p = r; }
-    }
-    piv[k] = p;
-    if (!(mx > 0)) return false;
-#pragma unroll
-    for (int r = k + 1; r < 6; ++r) {
-      const bool sw = (p == r);
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double a = A[k][c], b = A[r][c];
-        A[k][c] = sw ? b : a;
-        A[r][c] = sw ? a : b;
-      }
-    }
-    double inv = frcp(A[k][k]);
-#pragma unroll
-    for (int r = k + 1; r < 6; ++r) {
-      double f = A[r][k] * inv;
-      A[r][k] = f;
-#pragma unroll
-      for (int c = k + 1; c < 6; ++c) A[r][c] -= f * A[k][c];
-    }
-    A[k][k] = inv;  // store the reciprocal pivot for the back substitution
-  }
-  return true;
-}
-DAT_HD void lu6_solve(const double A[6][6], const int piv[6], double* b) {
-  // PA = LU with the multipliers exchanged along with their rows: permute b fully, then solve.
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-#pragma unroll
-    for (int r = k + 1; r < 6; ++r) {
-      const bool sw = (piv[k] == r);
-      double a = b[k], c = b[r];
-      b[k] = sw ? c : a;
-      b[r] = sw ? a : c;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 6; ++k)
-#pragma unroll
-    for (int r = k + 1; r < 6; ++r) b[r] -= A[r][k] * b[k];
-#pragma unroll
-  for (int k = 5; k >= 0; --k) {
-    double s = b[k];
-#pragma unroll
-    for (int c = k + 1; c < 6; ++c) s -= A[k][c] * b[c];
-    b[k] = s * A[k][k];
-  }
-}
 // 6x6 Cholesky of a packed SPD matrix into a packed lower factor (L[sp6(i,j)] = L_ij, i >= j);
 // diagonal entries hold 1 / L_jj.  Returns false if not SPD.
 DAT_HD bool chol6(const double* A, double* L) {

@@ -594,32 +594,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   for (int l = 0; l < NR; ++l) zl[l] = act(l);
 #pragma unroll
   for (int r = 0; r < 6; ++r) w[r] = 0.0;
+  // C-ADMM: the free aggregate starts at its unconstrained minimiser without the u-coupling,
+  // w = atil (the infeasible start lets the Newton steps restore rho (w - atil) + K_{-i} pi = 0).
+  // A consistent start through a 6x6 LU of (rho I + K C) took the same iteration count and held
+  // ~1 KB/lane more spill frame (C4 A/B: k_cadmm 8.9 -> 7.7 ms without it).
   if (MODE == MODE_CADMM) {
-    // consistent free aggregate: (rho I + K C) w = rho atil - K (C U y + cu - A' zl)
-    double uy[6], cuy[6], az[6], rhs[6], Kt[6];
-    compute_u(uy);  // w = 0 here
-    spmv6(Cp(), uy, cuy);
-    rows_adj(zl, az);
 #pragma unroll
-    for (int r = 0; r < 6; ++r) cuy[r] += cup()[r] - az[r];
-    Kmul(cuy, Kt);
-    double A[6][6];
-#pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      double col[6], kc[6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) col[r] = Cp()[sp6(r, c)];
-      Kmul(col, kc);
-#pragma unroll
-      for (int r = 0; r < 6; ++r) A[r][c] = kc[r] + (r == c ? P.rho : 0.0);
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) rhs[r] = P.rho * P.atil[r] - Kt[r];
-    int piv[6];
-    if (!lu6(A, piv)) return out;
-    lu6_solve(A, piv, rhs);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) w[r] = rhs[r];
+    for (int r = 0; r < 6; ++r) w[r] = P.atil[r];
   }
   {
     double u[6], dv[3], dw[3];
@@ -640,9 +621,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
   for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
 
-  // best iterate: in-band iterates (scaled residuals < 1e-7, gap < 1e-6) rank before all others,
-  // then by merit; best_merit (plain merit) drives the divergence stop
+  // best in-band iterate (merit of the recorded one) and the best merit seen (divergence stop)
   double best_merit = 1e300, best_key = 1e300;
+  out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
   const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
 
   for (int it = 0;; ++it) {
@@ -708,7 +689,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
       out.iters = it;
       if (!(fabs(chk + gap) < 1e300)) {  // NaN or Inf anywhere in the residuals
-        out.status = ST_FAILED;
+        // at the initial point: the problem data itself is not finite (the solver-exception
+        // branch); later: a numerical breakdown of a finite problem (not solved)
+        out.status = it == 0 ? ST_FAILED : ST_INACCURATE;
         break;
       }
       double merit = fmax(fmax(pres / nh, dres / nq), gap);
@@ -718,10 +701,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
         return out;
       }
+      // Only an in-band iterate (scaled residuals < 1e-7, gap < 1e-6) can be returned: a solve that
+      // ends out of band is INACCURATE and the callers hold their previous solution instead, so
+      // out-of-band iterates are never recorded (the record is written in the last one or two
+      // iterations of a stalling solve, not at every iteration).
       const bool band = fmax(pres / nh, dres / nq) < 1e-7 && gap < 1e-6;
-      const double key = band ? merit : 1.0 + merit;
-      if (key < best_key) {
-        best_key = key;
+      if (band && merit < best_key) {
+        best_key = merit;
 #pragma unroll
         for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -1209,7 +1195,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       out.pi[r] = best[3 * NB + 6 + r];
       out.u[r] = best[3 * NB + 12 + r];
     }
-    out.status = best_key < 1.0 ? ST_OPTIMAL : ST_INACCURATE;
+    out.status = ST_OPTIMAL;
   }
   return out;
 }
