@@ -211,25 +211,6 @@ DAT_HD bool chol6_lower(const double* A, double* L) {
   }
   return true;
 }
-// o = L v / o = L' v for a packed lower factor with true diagonal (o may not alias v)
-DAT_HD void trmv6(const double* L, const double* v, double* o) {
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k <= r; ++k) s += L[sp6(r, k)] * v[k];
-    o[r] = s;
-  }
-}
-DAT_HD void trmtv6(const double* L, const double* v, double* o) {
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    double s = 0.0;
-#pragma unroll
-    for (int k = r; k < 6; ++k) s += L[sp6(k, r)] * v[k];
-    o[r] = s;
-  }
-}
 // N = I + L' T L (packed) for a packed lower factor L with true diagonal and a packed symmetric T:
 // column c of T L, then the upper triangle of column c of L' (T L).
 DAT_HD void ltl_plus_identity(const double* L, const double* T, double* N) {
@@ -267,6 +248,32 @@ DAT_HD void chol6_solve(const double* L, double* b) {
     for (int k = i + 1; k < 6; ++k) s -= L[sp6(k, i)] * b[k];
     b[i] = s * L[sp6(i, i)];
   }
+}
+
+// P = Lm N^-1 Lm' (packed) from the packed lower factor Lm (true diagonal) of M and the Cholesky
+// factor Ln of N (reciprocal diagonal, chol6): with X = Lm Ln^-T (row r: Ln x = Lm[r, :]'), P = X X'.
+// The IPM keeps P (21 doubles) instead of Lm and Ln (42) through the Newton solves of an iteration;
+// the corrector's iterative refinement absorbs the accuracy of the explicit product.
+DAT_HD void schur_P(const double* Lm, const double* Ln, double* P) {
+  double X[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double s = (i <= r) ? Lm[sp6(r, i)] : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; ++k) s -= Ln[sp6(i, k)] * X[r][k];
+      X[r][i] = s * Ln[sp6(i, i)];
+    }
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = r; c < 6; ++c) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s += X[r][k] * X[c][k];
+      P[sp6(r, c)] = s;
+    }
 }
 
 // Rt_j = hat(r_com_j) Rl' ;  U_j = [I; Rt_j] maps an agent force to its (force, CoM moment) pair

@@ -779,11 +779,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     }
     if (!okc) break;
     // M = Lm Lm' (Cholesky; M is SPD: C carries k_f, k_m > 0) and, for CADMM / CENT, the Cholesky
-    // factor Ln of the SPD matrix N = I + Lm' T Lm, so that (I + M T)^-1 M = Lm N^-1 Lm'.  N has
-    // every eigenvalue >= 1 however large active rows make M, so the solve stays well conditioned
-    // without a pivoted nonsymmetric LU (and needs 42 doubles of factors instead of 57 + pivots).
+    // factor Ln of the SPD matrix N = I + Lm' T Lm, so that (I + M T)^-1 M = Lm N^-1 Lm' =: P.  N has
+    // every eigenvalue >= 1 however large active rows make M, so the factorisation stays well
+    // conditioned without a pivoted nonsymmetric LU; only P (21 doubles) is kept for the solves.
     // DD: Lm alone (reciprocal diagonal, for chol6_solve).
-    double Lm[21], Ln[21];
+    double Lm[21];  // DD: Cholesky factor of M;  CADMM / CENT: P = Lm N^-1 Lm' (schur_P)
     {
       double Mm[21];
       // M = C + sum_l (z/s) a_l a_l' (u-space, packed), assembled in (dvl, dwl) coordinates
@@ -841,9 +841,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int k = 0; k < NB; ++k) add_UDUt(T, rt.get(k), Dinv[k], 1.0);
         }
-        double Nn[21];
+        double Nn[21], Ln[21];
         ltl_plus_identity(Lm, T, Nn);
         if (!chol6(Nn, Ln)) break;
+        double Pm[21];
+        schur_P(Lm, Ln, Pm);
+#pragma unroll
+        for (int k = 0; k < 21; ++k) Lm[k] = Pm[k];
       }
     }
 
@@ -894,11 +898,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
             yv[r] += g6[r] * irho;
           }
         }
-        // tau = (I + M T)^-1 M yv = Lm N^-1 Lm' yv
-        double tau[6], xs[6];
-        trmtv6(Lm, yv, xs);
-        chol6_solve(Ln, xs);
-        trmv6(Lm, xs, tau);
+        // tau = (I + M T)^-1 M yv = Lm N^-1 Lm' yv = P yv
+        double tau[6];
+        spmv6(Lm, yv, tau);
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
           double t[3], v[3];
