@@ -140,33 +140,60 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 // LDS layout of one 64-lane block (G = floor(64/n) scenarios).  Per-lane records use an odd
 // stride in doubles so that the 32 lanes of a ds_read_b64 group fall on distinct bank pairs.
 //   fbar G x 3n    consensus mean
-//   Rt   G x 9n    hat(r_com_j) Rl'              red  64 x RDS (9)  per-lane exchange slots
-//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)
-//   env  EnvLds image (structure of arrays over the 64 lanes; env classes only)   done G ints
-// (n = 6: 19.6 KB without, 39.6 KB with the env image, so four wavefronts fit a CU's 160 KB.)
+//   Rt   G x 9n    hat(r_com_j) Rl'
+//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)            done / sid 64 + 64 ints
+//   area, laid out per env class:
+//     rows  the IPM's row state (RowLds: s, z, zw of NR slots x 64 lanes, 3 NR x 64 doubles); the
+//           consensus exchange slots red (64 x RDS) alias it: they are used only between solves
+//     env   EnvLdsN image of the class's env slots (structure of arrays over the 64 lanes)
+// The row state goes to LDS for every class whose image fits the 40 KB a wavefront may hold at
+// four wavefronts per CU (cadmm_rows_lds); otherwise it stays in registers.  n = 6: class 0
+// 19.9 KB, 1 27.1 KB, 2 37.8 KB (rows in LDS), 3 40.4 KB (rows in registers: 13 slots).
 constexpr int RDS = 9;
+constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
+__host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
+__host__ __device__ inline size_t cadmm_fixed_bytes(int n) {
+  const int G = 64 / n;
+  return sizeof(double) * ((size_t)G * 12 * n) + sizeof(QPShared) * (size_t)G + sizeof(int) * 128;
+}
+__host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
+  const size_t rows = lrows ? (size_t)row_lds_doubles(cadmm_nr(cls)) : 0;
+  return (rows > 64 * RDS ? rows : 64 * RDS) + (size_t)env_lds_doubles(class_env_rows(cls));
+}
+// row state of class cls in LDS: classes 0 and 1 always (their images fit the budget for n >= 3),
+// class 2 when it fits, class 3 (13 slots) never
+__host__ __device__ inline bool cadmm_rows_lds(int n, int cls) {
+  if (cls >= NCLS - 1) return false;
+  if (cls < 2) return true;
+  return cadmm_fixed_bytes(n) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
+}
+__host__ __device__ inline size_t cadmm_lds_bytes(int n) {
+  size_t m = 0;
+  for (int c = 0; c < NCLS; ++c) {
+    const size_t b = cadmm_fixed_bytes(n) + sizeof(double) * cadmm_area_doubles(c, cadmm_rows_lds(n, c));
+    m = b > m ? b : m;
+  }
+  return m;
+}
 struct CadmmLds {
-  double *fbar, *Rt, *red;
+  double *fbar, *Rt, *red, *rows;
   QPShared* sh;
   double* env;
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
 };
-__host__ __device__ inline size_t cadmm_lds_bytes(int n, bool env) {
-  const int G = 64 / n;
-  return sizeof(double) * ((size_t)G * 3 * n + (size_t)G * 9 * n + 64 * RDS) +
-         sizeof(QPShared) * (size_t)G + (env ? sizeof(double) * ENV_LDS_DOUBLES : 0) + sizeof(int) * 128;
-}
-__device__ inline CadmmLds cadmm_carve(double* smem, int n, bool env) {
+__device__ inline CadmmLds cadmm_carve(double* smem, int n, int cls, bool lrows) {
   const int G = 64 / n;
   CadmmLds L;
   L.fbar = smem;
   L.Rt = L.fbar + G * 3 * n;
-  L.red = L.Rt + G * 9 * n;
-  L.sh = (QPShared*)(L.red + 64 * RDS);
-  L.env = (double*)(L.sh + G);
-  L.done = (int*)(L.env + (env ? ENV_LDS_DOUBLES : 0));
+  L.sh = (QPShared*)(L.Rt + G * 9 * n);
+  L.done = (int*)(L.sh + G);
   L.sid = L.done + 64;
+  L.rows = (double*)(L.sid + 64);
+  L.red = L.rows;
+  const int ra = lrows ? row_lds_doubles(cadmm_nr(cls)) : 0;
+  L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
   return L;
 }
 
@@ -325,7 +352,8 @@ struct WaveCounters {
 template <int CLS>
 __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr bool ENV = CLS > 0;
-  constexpr int NR = NBASE + class_env_rows(CLS);
+  constexpr int NR = cadmm_nr(CLS);
+  constexpr int NE = class_env_rows(CLS);
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
   const int G = 64 / n, NT = G * n;
@@ -334,13 +362,14 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   const int lsc = ls < G ? ls : 0;
   const int cnt = a.scount[CLS], first = a.scount[NCLS + CLS];
   if (cnt == 0) return;
-  CadmmLds L = cadmm_carve(smem, n, true);
+  const bool lrows = cadmm_rows_lds(n, CLS);  // wave-uniform
+  CadmmLds L = cadmm_carve(smem, n, CLS, lrows);
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * 9 * n;
   double* myred = L.red + lane * RDS;
   QPShared& S = L.sh[lsc];
   const LdsRef<QPShared> shr{L.sh, lsc};
-  const EnvLds err{L.env, lane};
+  const EnvLdsN<NE> err{L.env, lane};
   const RtLds rtr{L.Rt, lsc * 9 * n + 9 * i};
   if (lane < G) L.sid[lane] = -1;
   __syncthreads();
@@ -399,7 +428,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         }
         EnvRows E;
         set_env_rows(P, E, S, emask, lhs, rhs);
-        env_to_lds(L.env, lane, E);
+        env_to_lds<NE>(L.env, lane, E);
       }
     }
     // ---- one ADMM pass of every occupied slot
@@ -408,8 +437,21 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
-      IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                              IPM_TOL);
+      IPMOut o;
+      if constexpr (CLS < 2) {
+        o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL,
+                                         RowLds{L.rows, lane});
+      } else if constexpr (CLS == 2) {
+        if (lrows)
+          o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                           IPM_TOL, RowLds{L.rows, lane});
+        else
+          o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                           IPM_TOL);
+      } else {
+        o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                         IPM_TOL);
+      }
       wc.ipm += o.iters;
       it_lane = o.iters;
       wc.rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
@@ -1372,7 +1414,7 @@ int launch_hl(dat_handle* h) {
     hipLaunchKernelGGL(k_env_class, dim3(blocks), dim3(64), 0, h->stream, a);
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
-    hipLaunchKernelGGL(k_cadmm, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), cadmm_lds_bytes(n, true),
+    hipLaunchKernelGGL(k_cadmm, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), cadmm_lds_bytes(n),
                        h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
@@ -1507,7 +1549,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     return fail(m);
   }
   // LDS budgets
-  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n, true) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
+  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
   if (lds > 160 * 1024) {
     dat_destroy(h);
     return fail("dat_create: LDS budget exceeded");

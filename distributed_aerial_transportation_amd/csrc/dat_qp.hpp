@@ -86,10 +86,12 @@ struct EnvPlain {
 };
 // LDS image of the env rows of a 64-lane wavefront, structure of arrays so that the lanes of a
 // wavefront reading the same slot hit 64 consecutive doubles (bank-conflict free; a per-lane
-// struct with its 40-double stride maps 32 lanes onto 4 banks):
-//   a_j[c] of lane l at [(3 j + c) * 64 + l],  b_j at [(3 DAT_NENV + j) * 64 + l].
-constexpr int ENV_LDS_DOUBLES = 4 * DAT_NENV * 64;
-struct EnvLds {
+// struct with its 40-double stride maps 32 lanes onto 4 banks), NE env slots:
+//   a_j[c] of lane l at [(3 j + c) * 64 + l],  b_j at [(3 NE + j) * 64 + l].
+__host__ __device__ constexpr int env_lds_doubles(int NE) { return 4 * NE * 64; }
+constexpr int ENV_LDS_DOUBLES = env_lds_doubles(DAT_NENV);
+template <int NE>
+struct EnvLdsN {
   const double* base;
   int lane;
   __device__ double a(int j, int c) const {
@@ -104,15 +106,18 @@ struct EnvLds {
 #ifndef DAT_LDS_HOIST
     __asm__ volatile("" : "+v"(l));
 #endif
-    return base[(3 * DAT_NENV + j) * 64 + l];
+    return base[(3 * NE + j) * 64 + l];
   }
 };
+using EnvLds = EnvLdsN<DAT_NENV>;
+// the first NE slots of E (set_env_rows compacts the active rows to the front)
+template <int NE = DAT_NENV>
 DAT_HD void env_to_lds(double* base, int lane, const EnvRows& E) {
 #pragma unroll
-  for (int j = 0; j < DAT_NENV; ++j) {
+  for (int j = 0; j < NE; ++j) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) base[(3 * j + c) * 64 + lane] = E.a[j][c];
-    base[(3 * DAT_NENV + j) * 64 + lane] = E.b[j];
+    base[(3 * NE + j) * 64 + lane] = E.b[j];
   }
 }
 
@@ -454,6 +459,43 @@ DAT_HD double soc_step(const double* x, const double* d) {
   return 1e300;
 }
 
+// Per-row IPM state (slack s_l, dual z_l, Newton row term zw_l of each row slot).  RowRegs keeps
+// it in registers; RowLds in a structure-of-arrays LDS image over the 64 lanes of a wavefront
+// (slot l of lane j: s at [l 64 + j], z at [(NR + l) 64 + j], zw at [(2 NR + l) 64 + j]; a
+// wavefront reading one slot touches 64 consecutive doubles, bank-conflict free), read and written
+// through an index the compiler cannot see through, so the rows cost no registers between uses.
+struct RowRegs {
+  template <int NR>
+  struct Store {
+    double s_[NR], z_[NR], w_[NR];
+    DAT_HD explicit Store(const RowRegs&) {}
+    DAT_HD double& s(int l) { return s_[l]; }
+    DAT_HD double& z(int l) { return z_[l]; }
+    DAT_HD double& w(int l) { return w_[l]; }
+  };
+};
+struct RowLds {
+  double* base;
+  int lane;
+  template <int NR>
+  struct Store {
+    double* base;
+    int lane;
+    __device__ explicit Store(const RowLds& r) : base(r.base), lane(r.lane) {}
+    __device__ double& at(int k) {
+      int j = lane;
+#ifndef DAT_LDS_HOIST
+      __asm__ volatile("" : "+v"(j));
+#endif
+      return base[k * 64 + j];
+    }
+    __device__ double& s(int l) { return at(l); }
+    __device__ double& z(int l) { return at(NR + l); }
+    __device__ double& w(int l) { return at(2 * NR + l); }
+  };
+};
+__host__ __device__ constexpr int row_lds_doubles(int NR) { return 3 * NR * 64; }
+
 struct IPMOut {
   int status;
   int iters;
@@ -474,9 +516,9 @@ struct IPMOut {
 // row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
-template <int MODE, int NB, int NR, class SH, class ER, class RT>
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
-                        double y[NB][3], double w[6], double* best, int max_iter, double tol) {
+                        double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{}) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   IPMOut out;
   out.status = ST_FAILED;
@@ -521,12 +563,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     o[0] = im * gv[0]; o[1] = im * gv[1]; o[2] = im * gv[2];
     o[3] = t[0] + s[0]; o[4] = t[1] + s[1]; o[5] = t[2] + s[2];
   };
-  auto rows_adj = [&](const double* zz, double* o) {  // o = A' zz (u-space)
+  auto rows_adj = [&](auto zz, double* o) {  // o = A' zz (u-space); zz(l): row multiplier
     double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0};
 #pragma unroll
     for (int l = 0; l < NR; ++l) {
       double* g = l < NWROW ? gw : gv;
-      g[0] += zz[l] * ra(l, 0); g[1] += zz[l] * ra(l, 1); g[2] += zz[l] * ra(l, 2);
+      const double zv = zz(l);
+      g[0] += zv * ra(l, 0); g[1] += zv * ra(l, 1); g[2] += zv * ra(l, 2);
     }
     adj(gv, gw, o);
   };
@@ -550,7 +593,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   };
   const double mfz = P.min_fz, mxf = P.max_f;
   // primal residual of cone block k at the current iterate: G y + s - h
-  double sk[NB][9], zk[NB][9], sl[NR], zl[NR];
+  double sk[NB][9], zk[NB][9];
+  typename RW::template Store<NR> rst(rw);  // row slacks / duals / Newton row terms (registers or LDS)
+  auto SL = [&](int l) -> double& { return rst.s(l); };
+  auto ZL = [&](int l) -> double& { return rst.z(l); };
   auto rzk_of = [&](int k, double* o) {
     Gy(y[k], o);
 #pragma unroll
@@ -591,7 +637,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     zk[k][0] = 1.0; zk[k][1] = 1.0; zk[k][5] = 1.0;
   }
 #pragma unroll
-  for (int l = 0; l < NR; ++l) zl[l] = act(l);
+  for (int l = 0; l < NR; ++l) ZL(l) = act(l);
 #pragma unroll
   for (int r = 0; r < 6; ++r) w[r] = 0.0;
   // C-ADMM: the free aggregate starts at its unconstrained minimiser without the u-coupling,
@@ -607,7 +653,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     compute_u(u);
     lin(u, dv, dw);
 #pragma unroll
-    for (int l = 0; l < NR; ++l) sl[l] = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
+    for (int l = 0; l < NR; ++l) SL(l) = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
   }
 
   // scales for the relative stopping rule
@@ -637,7 +683,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       compute_u(u);
       lin(u, dv, dw);
       spmv6(Cp(), u, pi);
-      rows_adj(zl, az);
+      rows_adj(ZL, az);
 #pragma unroll
       for (int r = 0; r < 6; ++r) pi[r] += cup()[r] - az[r];
 #pragma unroll
@@ -682,10 +728,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        const double rl = sl[l] - (rowdot(l, dv, dw) + rb(l));
+        const double rl = SL(l) - (rowdot(l, dv, dw) + rb(l));
         pres = fmax(pres, fabs(rl));
         chk += rl;
-        gap += sl[l] * zl[l];
+        gap += SL(l) * ZL(l);
       }
       out.iters = it;
       if (!(fabs(chk + gap) < 1e300)) {  // NaN or Inf anywhere in the residuals
@@ -791,7 +837,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         double Xv[6] = {0, 0, 0, 0, 0, 0}, Xw[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int l = 0; l < NR; ++l) {
-          const double wgt = zl[l] * frcp(sl[l]);
+          const double wgt = ZL(l) * frcp(SL(l));
           double* X = l < NWROW ? Xw : Xv;
           const double a0 = ra(l, 0), a1 = ra(l, 1), a2 = ra(l, 2);
           X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
@@ -944,7 +990,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     // formed in place from the predictor's row direction ddva/ddwa and its zw).  Outputs: dy, dw,
     // du, scaled dz of the cones (dzs_k), lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k) and zw
     // (row dz is zw - (z/s) a.lin(du)).
-    double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9], zw[NR];
+    double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9];
+    auto ZW = [&](int l) -> double& { return rst.w(l); };
     // tks_k = W^-1 rz_k - lam \ rsk
     auto tks_of = [&](int k, double* t) {
       double rz[9];
@@ -968,16 +1015,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        const double is = frcp(sl[l]);
-        const double rzl = sl[l] - (rowdot(l, dv, dw) + rb(l));
+        const double is = frcp(SL(l));
+        const double rzl = SL(l) - (rowdot(l, dv, dw) + rb(l));
         double cadd = 0.0;
         if (corr) {
           const double a = rowdot(l, ddva, ddwa);
-          cadd = act(l) * ((-rzl + a) * (zw[l] - zl[l] * is * a) - sigmu);
+          cadd = act(l) * ((-rzl + a) * (ZW(l) - ZL(l) * is * a) - sigmu);
         }
-        zw[l] = (zl[l] * rzl - (sl[l] * zl[l] + cadd)) * is;
+        ZW(l) = (ZL(l) * rzl - (SL(l) * ZL(l) + cadd)) * is;
       }
-      rows_adj(zw, bu);
+      rows_adj(ZW, bu);
       core(bk, Rf, bu, true, false, dy, dwv, du);
       // the affine (predictor) direction only sets the step length, sigma and the corrector's
       // second-order term: it is used unrefined; the corrector -- the step actually taken -- is refined
@@ -1000,7 +1047,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0}, adz[6];
 #pragma unroll
           for (int l = 0; l < NR; ++l) {
-            const double dzl = zw[l] - zl[l] * frcp(sl[l]) * rowdot(l, ddv, ddw);
+            const double dzl = ZW(l) - ZL(l) * frcp(SL(l)) * rowdot(l, ddv, ddw);
             double* g = l < NWROW ? gw : gv;
             g[0] += dzl * ra(l, 0); g[1] += dzl * ra(l, 1); g[2] += dzl * ra(l, 2);
           }
@@ -1058,8 +1105,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     // row directions of the current Newton solution
     auto row_dirs = [&](int l, const double* ddv, const double* ddw, double& ds, double& dz) {
       const double a = rowdot(l, ddv, ddw);
-      ds = -(sl[l] - (rowdot(l, dv, dw) + rb(l))) + a;
-      dz = zw[l] - zl[l] * frcp(sl[l]) * a;
+      ds = -(SL(l) - (rowdot(l, dv, dw) + rb(l))) + a;
+      dz = ZW(l) - ZL(l) * frcp(SL(l)) * a;
     };
     auto step_len = [&]() {
       double a = 1e300;
@@ -1081,8 +1128,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
-        if (ds < 0) a = fmin(a, -sl[l] * frcp(ds));
-        if (dz < 0) a = fmin(a, -zl[l] * frcp(dz));
+        if (ds < 0) a = fmin(a, -SL(l) * frcp(ds));
+        if (dz < 0) a = fmin(a, -ZL(l) * frcp(dz));
       }
       return a;
     };
@@ -1101,7 +1148,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
-        g += (sl[l] + al * ds) * (zl[l] + al * dz);
+        g += (SL(l) + al * ds) * (ZL(l) + al * dz);
       }
       return g;
     };
@@ -1176,8 +1223,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
         row_dirs(l, ddv, ddw, ds, dz);
-        sl[l] += alpha * ds;
-        zl[l] += alpha * dz;
+        SL(l) += alpha * ds;
+        ZL(l) += alpha * dz;
       }
     }
   }
