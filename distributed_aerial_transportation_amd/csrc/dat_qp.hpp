@@ -66,23 +66,30 @@ struct PlainRef {
   const T* p;
   DAT_HD const T& get() const { return *p; }
 };
+// The opaque value is the record's 32-bit LDS address (computed once, outside the solver loops),
+// so an access costs one register copy and a ds_read with an immediate offset -- no index multiply,
+// no address add.
+#define DAT_LDS __attribute__((address_space(3)))
+template <class T>
+__device__ inline const DAT_LDS T* lds_opaque(const DAT_LDS T* p) {
+#ifndef DAT_LDS_HOIST
+  __asm__ volatile("" : "+v"(p));
+#endif
+  return p;
+}
 template <class T>
 struct LdsRef {
-  const T* base;
-  int idx;
-  __device__ const T& get() const {
-    int j = idx;
-#ifndef DAT_LDS_HOIST
-    __asm__ volatile("" : "+v"(j));
-#endif
-    return base[j];
-  }
+  const DAT_LDS T* p;
+  __device__ LdsRef(const T* b, int idx) : p((const DAT_LDS T*)(b + idx)) {}
+  __device__ const T& get() const { return *(const T*)lds_opaque(p); }
 };
 // env-row accessors: a(j, c), b(j) of env slot j
 struct EnvPlain {
   const EnvRows* p;
   DAT_HD double a(int j, int c) const { return p->a[j][c]; }
   DAT_HD double b(int j) const { return p->b[j]; }
+  DAT_HD void a3(int j, double* o) const { o[0] = p->a[j][0]; o[1] = p->a[j][1]; o[2] = p->a[j][2]; }
+  DAT_HD void ab(int j, double* o, double& bb) const { a3(j, o); bb = p->b[j]; }
 };
 // LDS image of the env rows of a 64-lane wavefront, structure of arrays so that the lanes of a
 // wavefront reading the same slot hit 64 consecutive doubles (bank-conflict free; a per-lane
@@ -92,21 +99,19 @@ __host__ __device__ constexpr int env_lds_doubles(int NE) { return 4 * NE * 64; 
 constexpr int ENV_LDS_DOUBLES = env_lds_doubles(DAT_NENV);
 template <int NE>
 struct EnvLdsN {
-  const double* base;
-  int lane;
-  __device__ double a(int j, int c) const {
-    int l = lane;
-#ifndef DAT_LDS_HOIST
-    __asm__ volatile("" : "+v"(l));
-#endif
-    return base[(3 * j + c) * 64 + l];
+  const DAT_LDS double* p;  // the lane's column
+  __device__ EnvLdsN(const double* b, int lane) : p((const DAT_LDS double*)(b + lane)) {}
+  __device__ const DAT_LDS double* col() const { return lds_opaque(p); }
+  __device__ double a(int j, int c) const { return col()[(3 * j + c) * 64]; }
+  __device__ double b(int j) const { return col()[(3 * NE + j) * 64]; }
+  // one opaque offset for the row's coefficients (and constant)
+  __device__ void a3(int j, double* o) const {
+    o[0] = a(j, 0); o[1] = a(j, 1); o[2] = a(j, 2);
   }
-  __device__ double b(int j) const {
-    int l = lane;
-#ifndef DAT_LDS_HOIST
-    __asm__ volatile("" : "+v"(l));
-#endif
-    return base[(3 * NE + j) * 64 + l];
+  __device__ void ab(int j, double* o, double& bb) const {
+    const DAT_LDS double* q = col();
+    o[0] = q[(3 * j) * 64]; o[1] = q[(3 * j + 1) * 64]; o[2] = q[(3 * j + 2) * 64];
+    bb = q[(3 * NE + j) * 64];
   }
 };
 using EnvLds = EnvLdsN<DAT_NENV>;
@@ -127,15 +132,9 @@ struct RtPtr {
   DAT_HD const double* get(int k) const { return p + 9 * k; }
 };
 struct RtLds {
-  const double* base;
-  int off;  // offset of block 0 in doubles
-  __device__ const double* get(int k) const {
-    int j = off;
-#ifndef DAT_LDS_HOIST
-    __asm__ volatile("" : "+v"(j));
-#endif
-    return base + j + 9 * k;
-  }
+  const DAT_LDS double* p;  // block 0
+  __device__ RtLds(const double* b, int off) : p((const DAT_LDS double*)(b + off)) {}
+  __device__ const double* get(int k) const { return (const double*)(lds_opaque(p) + 9 * k); }
 };
 
 template <int NB>
@@ -479,19 +478,18 @@ struct RowLds {
   int lane;
   template <int NR>
   struct Store {
-    double* base;
-    int lane;
-    __device__ explicit Store(const RowLds& r) : base(r.base), lane(r.lane) {}
-    __device__ double& at(int k) {
-      int j = lane;
+    DAT_LDS double* p;  // the lane's column
+    __device__ explicit Store(const RowLds& r) : p((DAT_LDS double*)(r.base + r.lane)) {}
+    __device__ DAT_LDS double& at(int k) {
+      DAT_LDS double* q = p;
 #ifndef DAT_LDS_HOIST
-      __asm__ volatile("" : "+v"(j));
+      __asm__ volatile("" : "+v"(q));
 #endif
-      return base[k * 64 + j];
+      return q[k * 64];
     }
-    __device__ double& s(int l) { return at(l); }
-    __device__ double& z(int l) { return at(NR + l); }
-    __device__ double& w(int l) { return at(2 * NR + l); }
+    __device__ DAT_LDS double& s(int l) { return at(l); }
+    __device__ DAT_LDS double& z(int l) { return at(NR + l); }
+    __device__ DAT_LDS double& w(int l) { return at(2 * NR + l); }
   };
 };
 __host__ __device__ constexpr int row_lds_doubles(int NR) { return 3 * NR * 64; }
@@ -543,10 +541,35 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.a(l >= NBASE ? l - NBASE : 0, c);
   };
   auto rb = [&](int l) -> double { return l < NBASE ? sh.get().bb[l < NBASE ? l : 0] : er.b(l >= NBASE ? l - NBASE : 0); };
+  // row coefficients a_l (one opaque access per row)
+  auto ra3 = [&](int l, double* a) {
+    if (l < NBASE) {
+      const int b = l < NBASE ? l : 0;
+      a[0] = sh.get().ba[b][0]; a[1] = sh.get().ba[b][1]; a[2] = sh.get().ba[b][2];
+    } else {
+      er.a3(l >= NBASE ? l - NBASE : 0, a);
+    }
+  };
   // row value a_l . (dvl or dwl) of the linear map of u
   auto rowdot = [&](int l, const double* dv, const double* dw) -> double {
     const double* x = l < NWROW ? dw : dv;
-    return ra(l, 0) * x[0] + ra(l, 1) * x[1] + ra(l, 2) * x[2];
+    double a[3];
+    ra3(l, a);
+    return a[0] * x[0] + a[1] * x[1] + a[2] * x[2];
+  };
+  // a_l . (dvl or dwl) + b_l
+  auto rowval = [&](int l, const double* dv, const double* dw) -> double {
+    const double* x = l < NWROW ? dw : dv;
+    double a[3], b;
+    if (l < NBASE) {
+      const QPShared& S = sh.get();
+      const int k = l < NBASE ? l : 0;
+      a[0] = S.ba[k][0]; a[1] = S.ba[k][1]; a[2] = S.ba[k][2];
+      b = S.bb[k];
+    } else {
+      er.ab(l >= NBASE ? l - NBASE : 0, a, b);
+    }
+    return (a[0] * x[0] + a[1] * x[1] + a[2] * x[2]) + b;
   };
   auto lin = [&](const double* u, double* dv, double* dw) {
     const QPShared& S = sh.get();
@@ -569,7 +592,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     for (int l = 0; l < NR; ++l) {
       double* g = l < NWROW ? gw : gv;
       const double zv = zz(l);
-      g[0] += zv * ra(l, 0); g[1] += zv * ra(l, 1); g[2] += zv * ra(l, 2);
+      double a[3];
+      ra3(l, a);
+      g[0] += zv * a[0]; g[1] += zv * a[1]; g[2] += zv * a[2];
     }
     adj(gv, gw, o);
   };
@@ -595,8 +620,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   // primal residual of cone block k at the current iterate: G y + s - h
   double sk[NB][9], zk[NB][9];
   typename RW::template Store<NR> rst(rw);  // row slacks / duals / Newton row terms (registers or LDS)
-  auto SL = [&](int l) -> double& { return rst.s(l); };
-  auto ZL = [&](int l) -> double& { return rst.z(l); };
+  auto SL = [&](int l) -> decltype(auto) { return rst.s(l); };
+  auto ZL = [&](int l) -> decltype(auto) { return rst.z(l); };
   auto rzk_of = [&](int k, double* o) {
     Gy(y[k], o);
 #pragma unroll
@@ -653,7 +678,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     compute_u(u);
     lin(u, dv, dw);
 #pragma unroll
-    for (int l = 0; l < NR; ++l) SL(l) = fmax(rowdot(l, dv, dw) + rb(l), 1.0);
+    for (int l = 0; l < NR; ++l) SL(l) = fmax(rowval(l, dv, dw), 1.0);
   }
 
   // scales for the relative stopping rule
@@ -728,7 +753,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        const double rl = SL(l) - (rowdot(l, dv, dw) + rb(l));
+        const double rl = SL(l) - (rowval(l, dv, dw));
         pres = fmax(pres, fabs(rl));
         chk += rl;
         gap += SL(l) * ZL(l);
@@ -839,7 +864,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         for (int l = 0; l < NR; ++l) {
           const double wgt = ZL(l) * frcp(SL(l));
           double* X = l < NWROW ? Xw : Xv;
-          const double a0 = ra(l, 0), a1 = ra(l, 1), a2 = ra(l, 2);
+          double a3v[3];
+          ra3(l, a3v);
+          const double a0 = a3v[0], a1 = a3v[1], a2 = a3v[2];
           X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
           X[3] += wgt * a1 * a1; X[4] += wgt * a1 * a2; X[5] += wgt * a2 * a2;
         }
@@ -991,7 +1018,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     // du, scaled dz of the cones (dzs_k), lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k) and zw
     // (row dz is zw - (z/s) a.lin(du)).
     double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9];
-    auto ZW = [&](int l) -> double& { return rst.w(l); };
+    auto ZW = [&](int l) -> decltype(auto) { return rst.w(l); };
     // tks_k = W^-1 rz_k - lam \ rsk
     auto tks_of = [&](int k, double* t) {
       double rz[9];
@@ -1016,7 +1043,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         const double is = frcp(SL(l));
-        const double rzl = SL(l) - (rowdot(l, dv, dw) + rb(l));
+        const double rzl = SL(l) - (rowval(l, dv, dw));
         double cadd = 0.0;
         if (corr) {
           const double a = rowdot(l, ddva, ddwa);
@@ -1049,7 +1076,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           for (int l = 0; l < NR; ++l) {
             const double dzl = ZW(l) - ZL(l) * frcp(SL(l)) * rowdot(l, ddv, ddw);
             double* g = l < NWROW ? gw : gv;
-            g[0] += dzl * ra(l, 0); g[1] += dzl * ra(l, 1); g[2] += dzl * ra(l, 2);
+            double a[3];
+            ra3(l, a);
+            g[0] += dzl * a[0]; g[1] += dzl * a[1]; g[2] += dzl * a[2];
           }
           adj(gv, gw, adz);
 #pragma unroll
@@ -1105,7 +1134,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     // row directions of the current Newton solution
     auto row_dirs = [&](int l, const double* ddv, const double* ddw, double& ds, double& dz) {
       const double a = rowdot(l, ddv, ddw);
-      ds = -(SL(l) - (rowdot(l, dv, dw) + rb(l))) + a;
+      ds = -(SL(l) - (rowval(l, dv, dw))) + a;
       dz = ZW(l) - ZL(l) * frcp(SL(l)) * a;
     };
     auto step_len = [&]() {

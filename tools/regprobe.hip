@@ -22,7 +22,7 @@ __global__ __launch_bounds__(64) void probe_ipm_cadmm(const double* prm, const d
   lane_cadmm_dynamic(P, prm, 6, lane % 6, rt, lam + 18 * lane, fb, 1.0);
   P.emask = NR > NBASE ? 1u : 0u;
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(LdsRef<QPShared>{sh, 0}, EnvLds{env, lane}, RtLds{rt, 9 * (lane % 6)}, P,
+  IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(LdsRef<QPShared>{sh, lane / 6}, EnvLds{env, lane}, RtLds{rt, 9 * (lane % 6)}, P,
                                           prm + DAT_P_FEQ(6), y, w, best + 21 * lane, 50, 1e-10);
   double* o8 = out + 16 * lane;
   for (int c = 0; c < 3; ++c) o8[c] = y[0][c];
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(64) void probe_ipm_cadmm_lrows(const double* prm, c
   lane_cadmm_dynamic(P, prm, 6, lane % 6, rt, lam + 18 * lane, fb, 1.0);
   P.emask = NR > NBASE ? 1u : 0u;
   double y[1][3], w[6];
-  IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(LdsRef<QPShared>{sh, 0}, EnvLds{env, lane}, RtLds{rt, 9 * (lane % 6)}, P,
+  IPMOut o = ipm_solve<MODE_CADMM, 1, NR>(LdsRef<QPShared>{sh, lane / 6}, EnvLds{env, lane}, RtLds{rt, 9 * (lane % 6)}, P,
                                           prm + DAT_P_FEQ(6), y, w, best + 21 * lane, 50, 1e-10, RowLds{rows, lane});
   double* o8 = out + 16 * lane;
   for (int c = 0; c < 3; ++c) o8[c] = y[0][c];
