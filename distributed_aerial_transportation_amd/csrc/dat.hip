@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 #include <algorithm>
@@ -146,9 +147,10 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 //     rows  the IPM's row state (RowLds: s, z, zw of NR slots x 64 lanes, 3 NR x 64 doubles); the
 //           consensus exchange slots red (64 x RDS) alias it: they are used only between solves
 //     env   EnvLdsN image of the class's env slots (structure of arrays over the 64 lanes)
-// The row state goes to LDS for every class whose image fits the 40 KB a wavefront may hold at
-// four wavefronts per CU (cadmm_rows_lds); otherwise it stays in registers.  n = 6: class 0
-// 19.9 KB, 1 27.1 KB, 2 37.8 KB (rows in LDS), 3 40.4 KB (rows in registers: 13 slots).
+// The row state goes to LDS for classes 1 and 2 when their image fits the 40 KB a wavefront may
+// hold at four wavefronts per CU (cadmm_rows_lds); class 0 (3 slots) and class 3 (13 slots) keep it
+// in registers.  n = 6: class 0 19.9 KB, 1 27.1 KB, 2 37.8 KB, 3 40.4 KB (C4 A/B, k_cadmm ms:
+// rows of classes 0-2 in LDS 5.53, classes 1-2 5.45, class 2 only 5.51).
 constexpr int RDS = 9;
 constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
@@ -160,11 +162,15 @@ __host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
   const size_t rows = lrows ? (size_t)row_lds_doubles(cadmm_nr(cls)) : 0;
   return (rows > 64 * RDS ? rows : 64 * RDS) + (size_t)env_lds_doubles(class_env_rows(cls));
 }
-// row state of class cls in LDS: classes 0 and 1 always (their images fit the budget for n >= 3),
-// class 2 when it fits, class 3 (13 slots) never
+// row state of class cls in LDS: classes ROWLDS_MIN_CLS .. 2 when the image fits the budget; class 3
+// (13 slots) never.  Few row slots are cheaper in registers: an LDS row access costs a register
+// copy and an LDS round trip, which pays only once the rows would otherwise spill.
+#ifndef DAT_ROWLDS_MIN_CLS
+#define DAT_ROWLDS_MIN_CLS 1
+#endif
+constexpr int ROWLDS_MIN_CLS = DAT_ROWLDS_MIN_CLS;
 __host__ __device__ inline bool cadmm_rows_lds(int n, int cls) {
-  if (cls >= NCLS - 1) return false;
-  if (cls < 2) return true;
+  if (cls >= NCLS - 1 || cls < ROWLDS_MIN_CLS) return false;
   return cadmm_fixed_bytes(n) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
 }
 __host__ __device__ inline size_t cadmm_lds_bytes(int n) {
@@ -438,10 +444,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
       double y[1][3], w[6];
       IPMOut o;
-      if constexpr (CLS < 2) {
-        o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL,
-                                         RowLds{L.rows, lane});
-      } else if constexpr (CLS == 2) {
+      if constexpr (CLS >= ROWLDS_MIN_CLS && CLS < NCLS - 1) {
         if (lrows)
           o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                            IPM_TOL, RowLds{L.rows, lane});
@@ -766,6 +769,10 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
 // DD step
 // ------------------------------------------------------------------------------------------------
 constexpr int DD_ES = 7, DD_RS = 5;
+// k_dd per-wavefront area: with a forest the env rows' LDS image; without one nothing (n = 6:
+// 27.0 KB, four wavefronts per CU -- the unused 20 KB image used to hold k_dd at three, C3 A/B
+// 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers (RowLds measured 26.2 ms).
+__host__ __device__ constexpr int dd_area_doubles(bool env) { return env ? ENV_LDS_DOUBLES : 0; }
 // k_dd_key: drain-order key of every scenario (previous step's DD iteration count, longest first),
 // sorted by k_bucket into one queue (class 0).
 __global__ void k_dd_key(KArgs a) {
@@ -794,8 +801,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* Rts = E + NT * DD_ES;     // G x 9n
   double* red = Rts + G * 9 * n;    // 64 x DD_RS
   QPShared* shs = (QPShared*)(red + 64 * DD_RS);  // G
-  double* envs = (double*)(shs + G);              // EnvLds image
-  int* sid = (int*)(envs + ENV_LDS_DOUBLES);      // G: scenario of the slot (-1 empty, -2 retired)
+  double* envs = (double*)(shs + G);              // EnvLds image (ENV only)
+  int* sid = (int*)(envs + dd_area_doubles(ENV));  // G: scenario of the slot (-1 empty, -2 retired)
   int* done = sid + 64;                           // G: the slot's scenario stopped in this pass
   QPShared& S = shs[lsc];
   double* myX = X + lane * 9;
@@ -881,10 +888,13 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       }
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
-      IPMOut o = ENV ? ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
-                                                  IPM_MAX_ITER, IPM_TOL)
-                     : ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                                    IPM_TOL);
+      IPMOut o;
+      if constexpr (ENV)
+        o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                       IPM_TOL);
+      else
+        o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                         IPM_TOL);
       my_ipm += o.iters;
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
@@ -1391,10 +1401,10 @@ KArgs kargs(dat_handle* h) {
   return a;
 }
 
-size_t dd_lds(int n) {
+size_t dd_lds(int n, bool env) {
   int G = 64 / n, NT = G * n;
   return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * DD_ES + (size_t)G * 9 * n + 64 * DD_RS) +
-         sizeof(QPShared) * (size_t)G + sizeof(double) * ENV_LDS_DOUBLES + sizeof(int) * 128;
+         sizeof(QPShared) * (size_t)G + sizeof(double) * dd_area_doubles(env) + sizeof(int) * 128;
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
@@ -1424,9 +1434,9 @@ int launch_hl(dat_handle* h) {
     int G = 64 / n;
     int blocks = (B + G - 1) / G;
     if (h->nforest > 0)
-      hipLaunchKernelGGL(k_dd<true>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n), h->stream, a);
+      hipLaunchKernelGGL(k_dd<true>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n, h->nforest > 0), h->stream, a);
     else
-      hipLaunchKernelGGL(k_dd<false>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n), h->stream, a);
+      hipLaunchKernelGGL(k_dd<false>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n, h->nforest > 0), h->stream, a);
   } else {
     int blocks = (B + 63) / 64;
     if (n == 3)
@@ -1509,6 +1519,8 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device) == hipSuccess && ncu > 0)
     h->persistent_blocks = 4 * ncu;  // k_cadmm: one wavefront per SIMD (register-bound), 4 SIMDs per CU
+  if (const char* e = getenv("DAT_WAVES_PER_CU"))  // development knob (occupancy experiments)
+    if (atoi(e) > 0 && ncu > 0) h->persistent_blocks = atoi(e) * ncu;
   const size_t B = c.batch, n = c.n, N3 = 3 * n;
   int rc = 0;
   rc |= dalloc(h, &h->state, B * h->S);
