@@ -38,13 +38,15 @@ DAT_HD void cross3(const double* a, const double* b, double* o) {
   double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
 }
-DAT_HD void mv3(const double* M, const double* v, double* o) {
+template <class PM>
+DAT_HD void mv3(PM M, const double* v, double* o) {
   double x = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
   double y = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
   double z = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
   o[0] = x; o[1] = y; o[2] = z;
 }
-DAT_HD void mtv3(const double* M, const double* v, double* o) {
+template <class PM>
+DAT_HD void mtv3(PM M, const double* v, double* o) {
   double x = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
   double y = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
   double z = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
@@ -127,7 +129,11 @@ DAT_HD constexpr int sp6(int r, int c) {
 DAT_HD constexpr int sp3(int r, int c) {
   return r <= c ? r * 3 - (r * (r - 1)) / 2 + (c - r) : c * 3 - (c * (c - 1)) / 2 + (r - c);
 }
-DAT_HD void spmv6(const double* A, const double* v, double* o) {
+template <class PA>
+DAT_HD void spmv6(PA Ap, const double* v, double* o) {
+  double A[21];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) A[k] = Ap[k];  // one read per entry (Ap may be a volatile LDS pointer)
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     double s = 0.0;
@@ -283,19 +289,24 @@ DAT_HD void make_Rt(const double* rcom, const double* Rl, double* Rt) {
   mmt3(H, Rl, Rt);
 }
 // U_j x = (x, Rt x)
-DAT_HD void U_apply(const double* Rt, const double* x, double* o) {
+template <class PR>
+DAT_HD void U_apply(PR Rt, const double* x, double* o) {
   o[0] = x[0]; o[1] = x[1]; o[2] = x[2];
   mv3(Rt, x, o + 3);
 }
 // U_j' v = v[0:3] + Rt' v[3:6]
-DAT_HD void Ut_apply(const double* Rt, const double* v, double* o) {
+template <class PR>
+DAT_HD void Ut_apply(PR Rt, const double* v, double* o) {
   mtv3(Rt, v + 3, o);
   o[0] += v[0]; o[1] += v[1]; o[2] += v[2];
 }
 // packed 6x6 M += scale * U D U' for U = [I; Rt] and packed symmetric 3x3 D
-DAT_HD void add_UDUt(double* M, const double* Rt, const double* D, double scale) {
+template <class PR>
+DAT_HD void add_UDUt(double* M, PR Rtp, const double* D, double scale) {
   double Df[9] = {D[0], D[1], D[2], D[1], D[3], D[4], D[2], D[4], D[5]};
-  double RD[9], RDR[9];
+  double Rt[9], RD[9], RDR[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Rt[k] = Rtp[k];  // one read per entry (Rtp may be a volatile LDS pointer)
   mm3(Rt, Df, RD);
   mmt3(RD, Rt, RDR);
 #pragma unroll

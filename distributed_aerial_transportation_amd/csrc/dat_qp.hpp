@@ -66,9 +66,10 @@ struct PlainRef {
   const T* p;
   DAT_HD const T& get() const { return *p; }
 };
-// The opaque value is the record's 32-bit LDS address (computed once, outside the solver loops),
-// so an access costs one register copy and a ds_read with an immediate offset -- no index multiply,
-// no address add.
+// LDS records are read through volatile address_space(3) pointers computed once, outside the
+// solver loops: every use is a ds_read with an immediate offset at the point of use (the compiler
+// may not hoist, merge or cache a volatile load), costing no register between uses and no address
+// arithmetic.
 #define DAT_LDS __attribute__((address_space(3)))
 template <class T>
 __device__ inline const DAT_LDS T* lds_opaque(const DAT_LDS T* p) {
@@ -79,9 +80,9 @@ __device__ inline const DAT_LDS T* lds_opaque(const DAT_LDS T* p) {
 }
 template <class T>
 struct LdsRef {
-  const DAT_LDS T* p;
-  __device__ LdsRef(const T* b, int idx) : p((const DAT_LDS T*)(b + idx)) {}
-  __device__ const T& get() const { return *(const T*)lds_opaque(p); }
+  const volatile DAT_LDS T* p;
+  __device__ LdsRef(const T* b, int idx) : p((const volatile DAT_LDS T*)(b + idx)) {}
+  __device__ const volatile DAT_LDS T& get() const { return *p; }
 };
 // env-row accessors: a(j, c), b(j) of env slot j
 struct EnvPlain {
@@ -102,14 +103,14 @@ struct EnvLdsN {
   const DAT_LDS double* p;  // the lane's column
   __device__ EnvLdsN(const double* b, int lane) : p((const DAT_LDS double*)(b + lane)) {}
   __device__ const DAT_LDS double* col() const { return lds_opaque(p); }
-  __device__ double a(int j, int c) const { return col()[(3 * j + c) * 64]; }
-  __device__ double b(int j) const { return col()[(3 * NE + j) * 64]; }
+  __device__ double a(int j, int c) const { return ((const volatile DAT_LDS double*)p)[(3 * j + c) * 64]; }
+  __device__ double b(int j) const { return ((const volatile DAT_LDS double*)p)[(3 * NE + j) * 64]; }
   // one opaque offset for the row's coefficients (and constant)
   __device__ void a3(int j, double* o) const {
     o[0] = a(j, 0); o[1] = a(j, 1); o[2] = a(j, 2);
   }
   __device__ void ab(int j, double* o, double& bb) const {
-    const DAT_LDS double* q = col();
+    const volatile DAT_LDS double* q = p;
     o[0] = q[(3 * j) * 64]; o[1] = q[(3 * j + 1) * 64]; o[2] = q[(3 * j + 2) * 64];
     bb = q[(3 * NE + j) * 64];
   }
@@ -132,9 +133,9 @@ struct RtPtr {
   DAT_HD const double* get(int k) const { return p + 9 * k; }
 };
 struct RtLds {
-  const DAT_LDS double* p;  // block 0
-  __device__ RtLds(const double* b, int off) : p((const DAT_LDS double*)(b + off)) {}
-  __device__ const double* get(int k) const { return (const double*)(lds_opaque(p) + 9 * k); }
+  const volatile DAT_LDS double* p;  // block 0
+  __device__ RtLds(const double* b, int off) : p((const volatile DAT_LDS double*)(b + off)) {}
+  __device__ const volatile DAT_LDS double* get(int k) const { return p + 9 * k; }
 };
 
 template <int NB>
@@ -480,16 +481,10 @@ struct RowLds {
   struct Store {
     DAT_LDS double* p;  // the lane's column
     __device__ explicit Store(const RowLds& r) : p((DAT_LDS double*)(r.base + r.lane)) {}
-    __device__ DAT_LDS double& at(int k) {
-      DAT_LDS double* q = p;
-#ifndef DAT_LDS_HOIST
-      __asm__ volatile("" : "+v"(q));
-#endif
-      return q[k * 64];
-    }
-    __device__ DAT_LDS double& s(int l) { return at(l); }
-    __device__ DAT_LDS double& z(int l) { return at(NR + l); }
-    __device__ DAT_LDS double& w(int l) { return at(2 * NR + l); }
+    __device__ volatile DAT_LDS double& at(int k) { return ((volatile DAT_LDS double*)p)[k * 64]; }
+    __device__ volatile DAT_LDS double& s(int l) { return at(l); }
+    __device__ volatile DAT_LDS double& z(int l) { return at(NR + l); }
+    __device__ volatile DAT_LDS double& w(int l) { return at(2 * NR + l); }
   };
 };
 __host__ __device__ constexpr int row_lds_doubles(int NR) { return 3 * NR * 64; }
@@ -535,8 +530,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   const double irho = 1.0 / P.rho;
   const double im = sh.get().inv_mT;
   auto act = [&](int l) -> double { return ((mask >> l) & 1u) ? 1.0 : 0.0; };
-  auto Cp = [&]() -> const double* { return sh.get().C[var]; };
-  auto cup = [&]() -> const double* { return sh.get().cu[var]; };
+  auto Cp = [&]() { return &sh.get().C[var][0]; };
+  auto cup = [&]() { return &sh.get().cu[var][0]; };
   auto ra = [&](int l, int c) -> double {
     return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.a(l >= NBASE ? l - NBASE : 0, c);
   };
@@ -562,7 +557,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     const double* x = l < NWROW ? dw : dv;
     double a[3], b;
     if (l < NBASE) {
-      const QPShared& S = sh.get();
+      const auto& S = sh.get();
       const int k = l < NBASE ? l : 0;
       a[0] = S.ba[k][0]; a[1] = S.ba[k][1]; a[2] = S.ba[k][2];
       b = S.bb[k];
@@ -572,14 +567,14 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     return (a[0] * x[0] + a[1] * x[1] + a[2] * x[2]) + b;
   };
   auto lin = [&](const double* u, double* dv, double* dw) {
-    const QPShared& S = sh.get();
+    const auto& S = sh.get();
     double t[3];
     mv3(S.Bv, u + 3, t);
     dv[0] = im * u[0] + t[0]; dv[1] = im * u[1] + t[1]; dv[2] = im * u[2] + t[2];
     mv3(S.JTi, u + 3, dw);
   };
   auto adj = [&](const double* gv, const double* gw, double* o) {
-    const QPShared& S = sh.get();
+    const auto& S = sh.get();
     double t[3], s[3];
     mtv3(S.Bv, gv, t);
     mtv3(S.JTi, gw, s);
@@ -871,7 +866,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           X[3] += wgt * a1 * a1; X[4] += wgt * a1 * a2; X[5] += wgt * a2 * a2;
         }
         // Av = [im I, Bv];  Av' Xv Av = [[im^2 Xv, im Xv Bv], [., Bv' Xv Bv]];  Aw = [0, JTi]
-        const QPShared& S = sh.get();
+        const auto& S = sh.get();
         double XB[9], XJ[9];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -880,7 +875,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
             XB[3 * r + c] = Xv[sp3(r, 0)] * S.Bv[c] + Xv[sp3(r, 1)] * S.Bv[3 + c] + Xv[sp3(r, 2)] * S.Bv[6 + c];
             XJ[3 * r + c] = Xw[sp3(r, 0)] * S.JTi[c] + Xw[sp3(r, 1)] * S.JTi[3 + c] + Xw[sp3(r, 2)] * S.JTi[6 + c];
           }
-        const double* C = S.C[var];
+        const auto* C = &S.C[var][0];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -902,7 +897,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho)
         double T[21];
         if (MODE == MODE_CADMM) {
-          const double* K = sh.get().K;
+          const auto* K = &sh.get().K[0];
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
           // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
