@@ -10,7 +10,7 @@
 //   k_dd       DD control step: prices, agent QPs, consensus error, dual ascent through H^-1
 //              (control/rqp_dd.py:659-752).
 //   k_cent     centralized QP, one lane per scenario (control/rqp_centralized.py:436-448).
-//   k_rollout  low-level SO(3) PD + dynamics + Lie integration, one lane per scenario.
+//   k_rollout_agents  low-level SO(3) law + dynamics + Lie integration, one lane per agent.
 //   k_desired  forest desired-acceleration law (example/rqp_example.py:33-59).
 #include <hip/hip_runtime.h>
 
@@ -92,6 +92,7 @@ struct KArgs {
   double* err;
   unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
                                  // (C-ADMM: [CNT_STRIDE k + .] per env class k, cadmm_block<k>)
+  int G;                         // C-ADMM: scenario slots per k_cadmm wavefront (cadmm_slots)
   int* need;                     // C-ADMM: per-scenario sort key of the step (k_env_class)
   int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
   int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
@@ -154,8 +155,8 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 constexpr int RDS = 9;
 constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
-__host__ __device__ inline size_t cadmm_fixed_bytes(int n) {
-  const int G = 64 / n;
+// G: scenario slots per wavefront (cadmm_slots)
+__host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
   return sizeof(double) * ((size_t)G * 12 * n) + sizeof(QPShared) * (size_t)G + sizeof(int) * 128;
 }
 __host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
@@ -169,14 +170,14 @@ __host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
 #define DAT_ROWLDS_MIN_CLS 1
 #endif
 constexpr int ROWLDS_MIN_CLS = DAT_ROWLDS_MIN_CLS;
-__host__ __device__ inline bool cadmm_rows_lds(int n, int cls) {
+__host__ __device__ inline bool cadmm_rows_lds(int n, int G, int cls) {
   if (cls >= NCLS - 1 || cls < ROWLDS_MIN_CLS) return false;
-  return cadmm_fixed_bytes(n) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
+  return cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
 }
-__host__ __device__ inline size_t cadmm_lds_bytes(int n) {
+__host__ __device__ inline size_t cadmm_lds_bytes(int n, int G) {
   size_t m = 0;
   for (int c = 0; c < NCLS; ++c) {
-    const size_t b = cadmm_fixed_bytes(n) + sizeof(double) * cadmm_area_doubles(c, cadmm_rows_lds(n, c));
+    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_rows_lds(n, G, c));
     m = b > m ? b : m;
   }
   return m;
@@ -188,8 +189,7 @@ struct CadmmLds {
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
 };
-__device__ inline CadmmLds cadmm_carve(double* smem, int n, int cls, bool lrows) {
-  const int G = 64 / n;
+__device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool lrows) {
   CadmmLds L;
   L.fbar = smem;
   L.Rt = L.fbar + G * 3 * n;
@@ -223,9 +223,158 @@ __device__ inline int env_class_of(unsigned emask, const double lhs[DAT_NENV][3]
   return c;
 }
 
+// Env rows of the n agents of each scenario of a 64-lane block, computed cooperatively
+// (control/rqp_cadmm.py:307-373 via env_rows' arithmetic).  The payload capsule and the x-window of
+// candidate trees are the same for every agent of a scenario; only the camera-cone filter differs
+// (cos 100 deg: most agents see most trees).  Lane i of a scenario evaluates trees base + i of each
+// chunk of n candidates -- range test, capsule_tree distance and the CBF row, once per tree instead
+// of once per agent that sees it -- and publishes them in LDS; then every lane runs its own cone
+// filter and sorted insertion over the chunk in tree order.  Same per-tree arithmetic and insertion
+// order as env_rows (the rows are bitwise identical; test_gpu_env_rows / test_gpu_c4).
+// Must be called by every lane of the block (barriers inside).
+constexpr int ENV_CE = 8;  // published entry: in range, c.x, c.y, dd, l3[3], r1
+__device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, const double* trees, int ntree, int i,
+                                int ls, bool valid, double alpha_env, unsigned* mask, double lhs[DAT_NENV][3],
+                                double rhs[DAT_NENV], double* ent /* LDS: 64 x ENV_CE */) {
+  EnvOut out;
+  out.collision = 0;
+  out.min_env_dist = valid ? prm[DAT_P_VISR] : 0.0;
+  *mask = 0u;
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) { lhs[j][0] = lhs[j][1] = lhs[j][2] = 0.0; rhs[j] = 0.0; }
+  const bool any = valid && trees != nullptr && ntree > 0;
+  bool dead = !any;  // this agent keeps no row (it still evaluates its share of the trees)
+  double xl[3] = {0, 0, 0}, vl[3] = {0, 0, 0}, vdir[3] = {0, 0, 0}, seg[3] = {0, 0, 0}, ctr[3] = {0, 0, 0};
+  double h = 0.0, speed = 0.0, maxdec = 1.0, reach = 0.0, rc = 0.0, deps = 0.0, cosang = 0.0;
+  double cam[2] = {0, 0}, dir[2] = {0, 0};
+  int t0 = 0;
+  if (any) {
+    const double* xlp = st + DAT_S_XL(n);
+    const double* vlp = st + DAT_S_VL(n);
+    const double* Rl = st + DAT_S_RL(n);
+    for (int c = 0; c < 3; ++c) { xl[c] = xlp[c]; vl[c] = vlp[c]; }
+    maxdec = prm[DAT_P_MAXDEC];
+    rc = prm[DAT_P_COLR];
+    deps = prm[DAT_P_DISTEPS];
+    cosang = prm[DAT_P_COSCONE];
+    const double v2 = dot3(vl, vl);
+    h = 0.5 * v2 / maxdec;
+    speed = sqrt(v2);
+    ctr[0] = xl[0]; ctr[1] = xl[1]; ctr[2] = xl[2];
+    if (speed != 0.0) {
+      vdir[0] = vl[0] / speed; vdir[1] = vl[1] / speed; vdir[2] = vl[2] / speed;
+      seg[0] = h * vdir[0]; seg[1] = h * vdir[1]; seg[2] = h * vdir[2];
+      ctr[0] += 0.5 * seg[0]; ctr[1] += 0.5 * seg[1]; ctr[2] += 0.5 * seg[2];
+    }
+    const double* r = prm + DAT_P_R(n) + 3 * i;
+    double Rr[3];
+    mv3(Rl, r, Rr);
+    cam[0] = xl[0] + Rr[0];
+    cam[1] = xl[1] + Rr[1];
+    const double dx = cam[0] - xl[0], dy = cam[1] - xl[1];
+    const double nn = sqrt(dx * dx + dy * dy);
+    if (nn == 0.0) {
+      out.collision = 1;
+      dead = true;
+    } else {
+      dir[0] = dx / nn; dir[1] = dy / nn;
+    }
+    reach = prm[DAT_P_VISR] + DAT_BARK_RADIUS;
+    for (int len = ntree; len > 0;) {
+      int half = len >> 1;
+      if (trees[3 * (t0 + half)] < ctr[0] - reach) { t0 += half + 1; len -= half + 1; } else { len = half; }
+    }
+  }
+  double bd[DAT_NENV];
+#pragma unroll
+  for (int j = 0; j < DAT_NENV; ++j) bd[j] = 1e300;
+  int cnt = 0;
+  double dmin = 1e300;
+  double* mine = ent + (size_t)threadIdx.x * ENV_CE;
+  const double* grp = ent + (size_t)(ls * n) * ENV_CE;
+  for (int base = t0;; base += n) {
+    // this lane's tree of the chunk
+    const int t = base + i;
+    const bool cand = any && t < ntree && trees[3 * t] <= ctr[0] + reach;
+    double e[ENV_CE] = {0, 0, 0, 1e300, 0, 0, 0, 0};
+    if (cand) {
+      const double* c = trees + 3 * t;
+      const double ex = ctr[0] - c[0], ey = ctr[1] - c[1], ez = ctr[2] - c[2];
+      if (!(sqrt(ex * ex + ey * ey + ez * ez) > prm[DAT_P_VISR] + DAT_BARK_RADIUS)) {
+        double p1[3], p2[3];
+        const double dd = capsule_tree(xl, seg, rc, c, p1, p2);
+        double l3[3] = {0, 0, 0}, r1 = 0.0;
+        if (dd > 1e-4 && speed > 0.0) {
+          double rel[3] = {p1[0] - xl[0], p1[1] - xl[1], p1[2] - xl[2]};
+          double proj = fmax(0.0, fmin(h, dot3(rel, vdir)));
+          double mt = sqrt(2.0 * (h - proj) / maxdec);
+          mt = fmax(0.0, speed / maxdec - mt);
+          if (mt < 1e-12 * speed / maxdec) mt = 0.0;
+          double nr[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+          double nn = sqrt(dot3(nr, nr));
+          nr[0] /= nn; nr[1] /= nn; nr[2] /= nn;
+          l3[0] = nr[0] * mt; l3[1] = nr[1] * mt; l3[2] = nr[2] * mt;
+          r1 = -alpha_env * (dd - deps) - dot3(nr, vl);
+        }
+        e[0] = 1.0; e[1] = c[0]; e[2] = c[1]; e[3] = dd;
+        e[4] = l3[0]; e[5] = l3[1]; e[6] = l3[2]; e[7] = r1;
+      }
+    }
+    // every lane of the block takes part in the barriers; the loop ends when no lane had a candidate
+    if (!__syncthreads_or(cand)) break;
+#pragma unroll
+    for (int k = 0; k < ENV_CE; ++k) mine[k] = e[k];
+    __syncthreads();
+    if (!dead) {
+      for (int j = 0; j < n; ++j) {  // the chunk in tree order
+        const double* q = grp + (size_t)j * ENV_CE;
+        if (q[0] == 0.0) continue;
+        const double tx = q[1] - cam[0], ty = q[2] - cam[1];
+        const double nn = sqrt(tx * tx + ty * ty);
+        if (nn > 0.0 && (tx / nn * dir[0] + ty / nn * dir[1]) < cosang) continue;
+        const double dd = q[3];
+        if (dd < 1e-4) out.collision = 1;
+        dmin = fmin(dmin, dd);
+        ++cnt;
+        int pos = 0;
+#pragma unroll
+        for (int jj = 0; jj < DAT_NENV; ++jj) pos += (bd[jj] <= dd) ? 1 : 0;
+        if (pos >= DAT_NENV) continue;
+#pragma unroll
+        for (int jj = DAT_NENV - 1; jj >= 1; --jj) {
+          if (jj > pos) {
+            bd[jj] = bd[jj - 1];
+            lhs[jj][0] = lhs[jj - 1][0]; lhs[jj][1] = lhs[jj - 1][1]; lhs[jj][2] = lhs[jj - 1][2];
+            rhs[jj] = rhs[jj - 1];
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < DAT_NENV; ++jj) {
+          if (jj == pos) {
+            bd[jj] = dd;
+            lhs[jj][0] = q[4]; lhs[jj][1] = q[5]; lhs[jj][2] = q[6];
+            rhs[jj] = q[7];
+          }
+        }
+      }
+    }
+    __syncthreads();  // the chunk is consumed before the next one is published
+  }
+  if (!dead && cnt > 0 && speed > 0.0) {
+    out.min_env_dist = dmin;
+    unsigned m = 0u;
+#pragma unroll
+    for (int j = 0; j < DAT_NENV; ++j)
+      if (bd[j] < 1e299 && bd[j] > 1e-4) m |= 1u << j;
+    *mask = m;
+  }
+  return out;
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_env_class(KArgs a) {
   __shared__ int nd[64], cl[64];
   __shared__ double md[64];
+  __shared__ double ent[64 * ENV_CE];
   const int n = a.n, G = 64 / n, NT = G * n;
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
@@ -233,14 +382,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   const bool valid = (lane < NT) && (sc < a.B);
   int need = 0, col = 0;
   double dist = 1e300;
+  const double* prm = valid ? prm_of(a, sc) : a.params;
+  const double* trees = nullptr;
+  int nt = 0;
+  if (valid) forest_of(a, sc, &trees, &nt);
+  unsigned emask;
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  EnvOut e = env_rows_coop(prm, n, valid ? a.state + (size_t)sc * a.S : nullptr, trees, nt, i, ls, valid,
+                           prm[DAT_P_AENVD], &emask, lhs, rhs, ent);
   if (valid) {
-    const double* prm = prm_of(a, sc);
-    const double* trees;
-    int nt;
-    unsigned emask;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    EnvOut e = env_rows(prm, n, a.state + (size_t)sc * a.S, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
     need = env_class_of(emask, lhs, rhs);
     col = e.collision;
     dist = e.min_env_dist;
@@ -362,14 +512,14 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr int NE = class_env_rows(CLS);
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
-  const int G = 64 / n, NT = G * n;
+  const int G = a.G, NT = G * n;  // G <= 64 / n scenario slots (cadmm_slots)
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
   const int lsc = ls < G ? ls : 0;
   const int cnt = a.scount[CLS], first = a.scount[NCLS + CLS];
   if (cnt == 0) return;
-  const bool lrows = cadmm_rows_lds(n, CLS);  // wave-uniform
-  CadmmLds L = cadmm_carve(smem, n, CLS, lrows);
+  const bool lrows = cadmm_rows_lds(n, G, CLS);  // wave-uniform
+  CadmmLds L = cadmm_carve(smem, n, G, CLS, lrows);
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * 9 * n;
   double* myred = L.red + lane * RDS;
@@ -1070,34 +1220,122 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
 // ------------------------------------------------------------------------------------------------
 // rollout / desired acceleration / warm start
 // ------------------------------------------------------------------------------------------------
-// NN > 0: team size known at compile time (every loop over agents unrolls, the state stays in
-// registers); NN = 0: any n <= NMAX from a.n (the state array then lives in scratch).
-template <int NN>
-__global__ __launch_bounds__(64) void k_rollout(KArgs a, int steps, double dt, const double* fdes) {
-  constexpr int NA = NN > 0 ? NN : NMAX;
-  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sc >= a.B) return;
-  const int n = NN > 0 ? NN : a.n;
-  const int S = DAT_STATE_SIZE(n);
-  const double* prm = prm_of(a, sc);
-  double st[DAT_STATE_SIZE(NA)];
-  double* g = a.state + (size_t)sc * a.S;
-  for (int k = 0; k < S; ++k) st[k] = g[k];
-  int cnt = a.counter[sc];
-  const double* fd = fdes + (size_t)sc * 3 * n;
-  for (int s = 0; s < steps; ++s) sim_step<NA>(prm, n, st, &cnt, fd, dt, a.ll_kind);
-  for (int k = 0; k < S; ++k) g[k] = st[k];
-  a.counter[sc] = cnt;
+// `steps` simulation steps (sim_step, system/rigid_quadrotor_payload.py:129-222) with one lane per (scenario, agent): G = floor(64/n) scenarios
+// per 64-lane block.  Lane i runs agent i's low-level law, rotational dynamics and attitude
+// integration; the payload's force / moment sums go through LDS and every lane of the scenario
+// integrates the payload identically (sums in agent order, the arithmetic of sim_step: bitwise the
+// same trajectory).  Per-lane state is one quadrotor plus the payload (~40 doubles), so nothing
+// spills and the kernel runs many wavefronts per SIMD, for any n (k_rollout<0> kept the whole state
+// of a large team in scratch).
+constexpr int RO_X = 6;  // per lane in LDS: u = f R e3 (3), hat(r_com) Rl' u (3)
+__global__ __launch_bounds__(64) void k_rollout_agents(KArgs a, int steps, double dt, const double* fdes) {
+  __shared__ double xs[64 * RO_X];
+  const int n = a.n, G = 64 / n, NT = G * n;
+  const int lane = threadIdx.x, ls = lane / n, i = lane - ls * n;
+  const int sc = blockIdx.x * G + ls;
+  const bool valid = lane < NT && sc < a.B;
+  const double* prm = valid ? prm_of(a, sc) : a.params;
+  double* g = valid ? a.state + (size_t)sc * a.S : nullptr;
+  double R[9], W[3], xl[3], vl[3], Rl[9], wl[3], fd[3];
+  int cnt = 0;
+  if (valid) {
+    for (int k = 0; k < 9; ++k) { R[k] = g[DAT_S_R(n) + 9 * i + k]; Rl[k] = g[DAT_S_RL(n) + k]; }
+    for (int c = 0; c < 3; ++c) {
+      W[c] = g[DAT_S_W(n) + 3 * i + c];
+      xl[c] = g[DAT_S_XL(n) + c];
+      vl[c] = g[DAT_S_VL(n) + c];
+      wl[c] = g[DAT_S_WL(n) + c];
+      fd[c] = fdes[(size_t)sc * 3 * n + 3 * i + c];
+    }
+    cnt = a.counter[sc];
+  }
+  const double* J = prm + DAT_P_J(n) + 9 * i;
+  const double* Ji = prm + DAT_P_JINV(n) + 9 * i;
+  double* mine = xs + lane * RO_X;
+  const double* grp = xs + ls * n * RO_X;
+  for (int s = 0; s < steps; ++s) {
+    double dw[3] = {0, 0, 0};
+    if (valid) {
+      double f, M[3], Jw[3], wJw[3], t[3];
+      ll_control_agent(R, W, J, fd, &f, M, a.ll_kind);
+      mv3(J, W, Jw);
+      cross3(W, Jw, wJw);
+      for (int c = 0; c < 3; ++c) t[c] = M[c] - wJw[c];
+      mv3(Ji, t, dw);
+      double u[3] = {R[2] * f, R[5] * f, R[8] * f};  // f R e3
+      double ub[3], m3[3];
+      mtv3(Rl, u, ub);
+      cross3(prm + DAT_P_RCOM(n) + 3 * i, ub, m3);
+      for (int c = 0; c < 3; ++c) { mine[c] = u[c]; mine[3 + c] = m3[c]; }
+    }
+    __syncthreads();
+    if (valid) {
+      double dvc[3] = {0, 0, 0}, mom[3] = {0, 0, 0};
+      for (int k = 0; k < n; ++k)
+        for (int c = 0; c < 3; ++c) { dvc[c] += grp[k * RO_X + c]; mom[c] += grp[k * RO_X + 3 + c]; }
+      const double mT = prm[DAT_P_MT];
+      const double* xc = prm + DAT_P_XCOM;
+      for (int c = 0; c < 3; ++c) dvc[c] /= mT;
+      dvc[2] -= DAT_GRAVITY;
+      double Jwl[3], wJwl[3], t[3], dwl[3];
+      mv3(prm + DAT_P_JT, wl, Jwl);
+      cross3(wl, Jwl, wJwl);
+      for (int c = 0; c < 3; ++c) t[c] = mom[c] - wJwl[c];
+      mv3(prm + DAT_P_JTI, t, dwl);
+      double a1[3], a2[3], a3[3], sum[3], Rs[3], dvl[3];
+      cross3(wl, xc, a1);
+      cross3(wl, a1, a2);
+      cross3(dwl, xc, a3);
+      for (int c = 0; c < 3; ++c) sum[c] = a2[c] + a3[c];
+      mv3(Rl, sum, Rs);
+      for (int c = 0; c < 3; ++c) dvl[c] = dvc[c] - Rs[c];
+      {
+        double v[3], E[9], Rn[9];
+        for (int c = 0; c < 3; ++c) v[c] = (W[c] + dw[c] * dt / 2.0) * dt;
+        exp3(v, E);
+        mm3(R, E, Rn);
+        for (int k = 0; k < 9; ++k) R[k] = Rn[k];
+        for (int c = 0; c < 3; ++c) W[c] += dw[c] * dt;
+      }
+      for (int c = 0; c < 3; ++c) {
+        xl[c] = xl[c] + vl[c] * dt + dvl[c] * dt * dt / 2.0;
+        vl[c] = vl[c] + dvl[c] * dt;
+      }
+      {
+        double v[3], E[9], Rn[9];
+        for (int c = 0; c < 3; ++c) v[c] = (wl[c] + dwl[c] * dt / 2.0) * dt;
+        exp3(v, E);
+        mm3(Rl, E, Rn);
+        for (int k = 0; k < 9; ++k) Rl[k] = Rn[k];
+        for (int c = 0; c < 3; ++c) wl[c] += dwl[c] * dt;
+      }
+      cnt += 1;
+      if (cnt >= 20) {  // _INTEGRATION_STEPS_PER_ROTATION_PROJECTION
+        polar3(Rl);
+        polar3(R);
+        cnt = 0;
+      }
+    }
+    __syncthreads();  // the sums are read before the next step overwrites them
+  }
+  if (valid) {
+    for (int k = 0; k < 9; ++k) g[DAT_S_R(n) + 9 * i + k] = R[k];
+    for (int c = 0; c < 3; ++c) g[DAT_S_W(n) + 3 * i + c] = W[c];
+    if (i == 0) {
+      for (int c = 0; c < 3; ++c) {
+        g[DAT_S_XL(n) + c] = xl[c];
+        g[DAT_S_VL(n) + c] = vl[c];
+        g[DAT_S_WL(n) + c] = wl[c];
+      }
+      for (int k = 0; k < 9; ++k) g[DAT_S_RL(n) + k] = Rl[k];
+      a.counter[sc] = cnt;
+    }
+  }
 }
 
 void launch_rollout(const KArgs& a, int B, hipStream_t stream, int steps, double dt, const double* fdes) {
-  const dim3 grid((B + 63) / 64), block(64);
-  if (a.n == 3)
-    hipLaunchKernelGGL(k_rollout<3>, grid, block, 0, stream, a, steps, dt, fdes);
-  else if (a.n == 6)
-    hipLaunchKernelGGL(k_rollout<6>, grid, block, 0, stream, a, steps, dt, fdes);
-  else
-    hipLaunchKernelGGL(k_rollout<0>, grid, block, 0, stream, a, steps, dt, fdes);
+  const int G = 64 / a.n;
+  hipLaunchKernelGGL(k_rollout_agents, dim3((B + G - 1) / G), dim3(64), 0, stream, a, steps, dt, fdes);
 }
 
 // RQPLowLevelController.control (control/rqp_centralized.py:518-535) at the current states: thrust
@@ -1331,6 +1569,20 @@ struct dat_handle {
   std::vector<void*> allocs;
 };
 
+// C-ADMM scenario slots per k_cadmm wavefront: floor(64/n), fewer when the batch would not give
+// every CU a wavefront.  A small batch is then spread one wavefront per CU (a wavefront's ADMM pass
+// waits for the slowest of fewer lanes).  Not further: wavefronts sharing a CU pair's instruction
+// cache at different points of the ~100 KB unrolled IPM slow each other down (C2, 1,024 scenarios,
+// target blocks 1024 / 256 / 64 / floor(64/n) packing: 14.7 / 13.0 / 14.4 / 14.2 ms per step).
+int cadmm_slots(const dat_handle* h, int B, int n) {
+  const int gmax = 64 / n;
+  int pb = h->persistent_blocks / 4 > 0 ? h->persistent_blocks / 4 : 1;
+  if (const char* e = getenv("DAT_SLOT_BLOCKS"))  // development knob (small-batch experiments)
+    if (atoi(e) > 0) pb = atoi(e);
+  const int g = (B + pb - 1) / pb;
+  return g < 1 ? 1 : (g > gmax ? gmax : g);
+}
+
 namespace {
 
 template <typename T>
@@ -1356,6 +1608,7 @@ KArgs kargs(dat_handle* h) {
   const dat_config& c = h->cfg;
   a.B = c.batch;
   a.n = c.n;
+  a.G = cadmm_slots(h, c.batch, c.n);
   a.P = h->P;
   a.S = h->S;
   a.ppp = h->ppp;
@@ -1424,7 +1677,8 @@ int launch_hl(dat_handle* h) {
     hipLaunchKernelGGL(k_env_class, dim3(blocks), dim3(64), 0, h->stream, a);
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
-    hipLaunchKernelGGL(k_cadmm, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), cadmm_lds_bytes(n),
+    const int Gc = a.G, cblocks = (B + Gc - 1) / Gc;
+    hipLaunchKernelGGL(k_cadmm, dim3(std::min(cblocks, h->persistent_blocks)), dim3(64), cadmm_lds_bytes(n, Gc),
                        h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
@@ -1561,7 +1815,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     return fail(m);
   }
   // LDS budgets
-  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
+  size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n, 64 / c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);
   if (lds > 160 * 1024) {
     dat_destroy(h);
     return fail("dat_create: LDS budget exceeded");
