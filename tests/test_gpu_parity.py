@@ -232,10 +232,12 @@ def test_gpu_centralized_golden():
     assert np.all(r.iters == -1)
 
 
-def test_gpu_rollout_matches_oracle():
+@pytest.mark.parametrize("n,B", [(3, 5), (4, 17), (6, 11), (16, 5)])
+def test_gpu_rollout_matches_oracle(n, B):
+    """k_rollout_agents (one lane per agent, floor(64/n) scenarios per block, partial last block)
+    over 45 steps (two polar projections) vs the oracle's dynamics and integration."""
     from distributed_aerial_transportation_amd import scenarios
 
-    n, B = 3, 5
     rng = np.random.default_rng(3)
     states = scenarios.perturbed_states(n, B, rng)
     eng = _eng("cadmm", n, B)
