@@ -35,6 +35,25 @@ constexpr int NBASE = 3;          // base slots shared by all agents of a scenar
 #define DAT_IPM_NREF 2
 #endif
 constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton solve
+// Initial point: cone / row slacks shifted to at least DAT_IPM_S0 inside, duals DAT_IPM_Z0 e.  The
+// agent QPs' multipliers are O(1e-2) at the solution; starting the duals and the slack margins there
+// instead of at 1 takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU
+// sweep over {0.01, 0.03, 0.1, 0.3, 1, 3, 10}^2, tools/ipm_init_sweep.py; same solutions to the
+// solver tolerance).
+#ifndef DAT_IPM_S0
+#define DAT_IPM_S0 0.03
+#endif
+#ifndef DAT_IPM_Z0
+#define DAT_IPM_Z0 0.03
+#endif
+// divergence stop (from the 5th iteration): merit above DAT_IPM_DIVERGE x the best seen.  A start
+// close to the boundary can raise the residuals by 1e3 in its first steps on a well-posed DD QP.
+#ifndef DAT_IPM_ETA
+#define DAT_IPM_ETA 0.999  // fraction of the step to the cone boundary (7.00 -> 5.23 -> 4.28 it/QP)
+#endif
+#ifndef DAT_IPM_DIVERGE
+#define DAT_IPM_DIVERGE 1e6
+#endif
 // refinement (corrector solve only) stops early once the linearised system's residual is within
 // 1e-12 of its right-hand side (C4 A/B: k_cadmm 11.0 ms with two passes per solve -> 8.9 ms)
 #ifndef DAT_IPM_REFINE_MODE
@@ -637,6 +656,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   };
 
   // ---------------- initial point
+  // agent QPs (C-ADMM, DD): the tuned start and step fraction; centralized (and the rigid payload on
+  // the same kernel, whose Jl^-1 ~ 50 grades the Newton systems): the conservative ones
+  constexpr double S0 = MODE == MODE_CENT ? 1.0 : DAT_IPM_S0;
+  constexpr double Z0 = MODE == MODE_CENT ? 1.0 : DAT_IPM_Z0;
+  constexpr double ETA = MODE == MODE_CENT ? 0.99 : DAT_IPM_ETA;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
 #pragma unroll
@@ -651,13 +675,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     double m1 = sk[k][0], m2 = sk[k][1] - sqrt(sk[k][2] * sk[k][2] + sk[k][3] * sk[k][3] + sk[k][4] * sk[k][4]);
     double m3 = sk[k][5] - sqrt(sk[k][6] * sk[k][6] + sk[k][7] * sk[k][7] + sk[k][8] * sk[k][8]);
     double mn = fmin(m1, fmin(m2, m3));
-    if (mn < 1e-3) { sk[k][0] += 1.0 - mn; sk[k][1] += 1.0 - mn; sk[k][5] += 1.0 - mn; }
+    if (mn < 1e-3) { sk[k][0] += S0 - mn; sk[k][1] += S0 - mn; sk[k][5] += S0 - mn; }
 #pragma unroll
     for (int j = 0; j < 9; ++j) zk[k][j] = 0.0;
-    zk[k][0] = 1.0; zk[k][1] = 1.0; zk[k][5] = 1.0;
+    zk[k][0] = Z0; zk[k][1] = Z0; zk[k][5] = Z0;
   }
 #pragma unroll
-  for (int l = 0; l < NR; ++l) ZL(l) = act(l);
+  for (int l = 0; l < NR; ++l) ZL(l) = Z0 * act(l);
 #pragma unroll
   for (int r = 0; r < 6; ++r) w[r] = 0.0;
   // C-ADMM: the free aggregate starts at its unconstrained minimiser without the u-coupling,
@@ -673,7 +697,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     compute_u(u);
     lin(u, dv, dw);
 #pragma unroll
-    for (int l = 0; l < NR; ++l) SL(l) = fmax(rowval(l, dv, dw), 1.0);
+    for (int l = 0; l < NR; ++l) SL(l) = fmax(rowval(l, dv, dw), S0);
   }
 
   // scales for the relative stopping rule
@@ -786,7 +810,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         }
       }
       best_merit = fmin(best_merit, merit);
-      if (merit > 1e3 * best_merit || it >= max_iter) {
+      if ((it >= 4 && merit > DAT_IPM_DIVERGE * best_merit) || it >= max_iter) {
         break;
       }
       if (it >= max_iter) break;
@@ -1215,7 +1239,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       lin(du, ddva, ddwa);
       newton(rsk, true, ddva, ddwa, sigmu);
     }
-    double alpha = fmin(1.0, 0.99 * step_len());
+    double alpha = fmin(1.0, ETA * step_len());
     // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
     // backtrack until the complementarity gap decreases
     const bool feasible = pres < 1e-8 * nh && dres < 1e-8 * nq;

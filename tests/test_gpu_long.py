@@ -37,7 +37,8 @@ pytestmark = pytest.mark.gpu
 # rows at step 2543 with its state ~3e-6 away from the reference's and f_des moves by 1.1e-5 there.
 # C-ADMM: the reference's own loop (QP tol 1e-10 vs 1e-11) keeps f_des within 1e-5 only to HL step
 # 667 (an ADMM iteration count flips at the 1e-2 threshold) and its states within 1e-4 to step 2280;
-# the GPU run holds both to step ~2446 (measured), and is required to within the reference's own.
+# the GPU run holds f_des to step ~2275 and its states to ~2450 (measured), and is required to within
+# the reference's own.
 REPRO_HL = {"cent": 3000, "cons": 2280, "dual": None}
 REPRO_HL_F = {"cent": 2500, "cons": 667, "dual": None}
 
@@ -78,7 +79,9 @@ def test_gpu_long_closed_loop_logs(tag, ct, capsys):
     # parity up to the reproducibility horizon
     Hl = H * 10 // int(d["hl_rel_freq"])  # log steps (log_freq = hl_rel_freq = 10)
     assert np.all(df[:HF] < 1e-5), (int(np.argmax(df[:HF] >= 1e-5)), df[:HF].max())
-    assert np.all(df[:H] < 2e-5)
+    # between HF and H the reference's own f_des is not reproducible to 1e-5 (its states are, to 1e-4):
+    # f_des within 1e-4 there (measured: C-ADMM leaves 1e-5 at step 2275, 2.3e-5 at 2280)
+    assert np.all(df[:H] < 1e-4), (int(np.argmax(df[:H] >= 1e-4)), df[:H].max())
     assert np.all(ds[: H // every] < 1e-4)
     if ct != "centralized":
         np.testing.assert_array_equal(np.array(logs["iter_seq"])[:HF], d["iters"][:HF])
