@@ -54,12 +54,16 @@ __host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c 
 // 6-9, 10-17, 18-33, >= 34), so that scenarios sharing a wavefront tend to need the same number of
 // ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
 // tail of the whole launch)
-constexpr int NIB = 8;
+constexpr int NAB = 8;   // ADMM / DD iteration bins
+constexpr int NPB = 4;   // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
+constexpr int NIB = NAB * NPB;
 __host__ __device__ inline int iter_bin(int it) {
   if (it <= 3) return it < 1 ? 0 : it - 1;
   const int lg = 31 - __builtin_clz((unsigned)(it - 2));  // floor(log2(it - 2)) >= 1
-  return 2 + lg < NIB - 1 ? 2 + lg : NIB - 1;
+  return 2 + lg < NAB - 1 ? 2 + lg : NAB - 1;
 }
+// IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8
+__host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
 constexpr int NKEY = NCLS * NIB;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
 constexpr int DAT_NCOUNTERS = NCLS * CNT_STRIDE;
@@ -94,6 +98,7 @@ struct KArgs {
                                  // (C-ADMM: [CNT_STRIDE k + .] per env class k, cadmm_block<k>)
   int G;                         // C-ADMM: scenario slots per k_cadmm wavefront (cadmm_slots)
   int* need;                     // C-ADMM: per-scenario sort key of the step (k_env_class)
+  int* ipmx;                     // C-ADMM: IPM iterations of the scenario's slowest agent QP, previous step
   int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
   int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
   int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
@@ -157,7 +162,7 @@ constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
 // G: scenario slots per wavefront (cadmm_slots)
 __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
-  return sizeof(double) * ((size_t)G * 12 * n) + sizeof(QPShared) * (size_t)G + sizeof(int) * 128;
+  return sizeof(double) * ((size_t)G * 12 * n) + sizeof(QPShared) * (size_t)G + sizeof(int) * 192;
 }
 __host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
   const size_t rows = lrows ? (size_t)row_lds_doubles(cadmm_nr(cls)) : 0;
@@ -188,6 +193,7 @@ struct CadmmLds {
   double* env;
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
+  int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
 };
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool lrows) {
   CadmmLds L;
@@ -196,7 +202,8 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool
   L.sh = (QPShared*)(L.Rt + G * 9 * n);
   L.done = (int*)(L.sh + G);
   L.sid = L.done + 64;
-  L.rows = (double*)(L.sid + 64);
+  L.wmx = L.sid + 64;
+  L.rows = (double*)(L.wmx + 64);
   L.red = L.rows;
   const int ra = lrows ? row_lds_doubles(cadmm_nr(cls)) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
@@ -418,8 +425,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
       c |= cl[ls * n + k];
       m = fmin(m, md[ls * n + k]);
     }
-    const int bin = iter_bin(a.iters[sc]);  // previous step's ADMM iterations
-    a.need[sc] = cls * NIB + (NIB - 1 - bin);               // longest first within the class
+    // previous step's ADMM iterations, then its slowest agent QP's IPM iterations: within a class the
+    // longest scenarios are claimed first and scenarios sharing a wavefront tend to need similar
+    // numbers of ADMM passes and of IPM iterations per pass (a pass lasts as long as its slowest lane)
+    const int bin = NPB * iter_bin(a.iters[sc]) + ipm_bin(a.ipmx[sc]);
+    a.need[sc] = cls * NIB + (NIB - 1 - bin);
     a.col[sc] = (unsigned char)c;
     a.mind[sc] = m;
   }
@@ -428,33 +438,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // Stable counting sort of the scenario ids by key (need[] in [0, NKEY)): list holds the ids of key
 // 0, then key 1, ...; count[c] / count[NCLS + c] = size / start of env class c (keys c NIB ..
 // c NIB + NIB - 1), count[2 NCLS + c] = 0 (queue head).  Within a class the key is the previous
-// step's ADMM iteration count, in decreasing order, so the longest scenarios are claimed first.
-// One BUCKET_T-thread workgroup; each thread owns a contiguous chunk of ids.
+// step's (ADMM iterations, slowest agent's IPM iterations) bin, in decreasing order, so the longest
+// scenarios are claimed first.  One BUCKET_T-thread workgroup; each thread owns a contiguous chunk of
+// ids and counts them in its own LDS column (O(ids), independent of the number of keys).
 // Grouping only changes which scenarios share a wavefront, never a scenario's arithmetic.
-constexpr int BUCKET_T = 512;
+constexpr int BUCKET_T = 128;
 __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int* list, int* count) {
-  __shared__ int s[NKEY][BUCKET_T + 1];
-  __shared__ int tot[NKEY];
+  __shared__ int s[NKEY][BUCKET_T + 1];  // s[k][t + 1]: ids of key k in thread t's chunk (then prefixes)
+  __shared__ int tot[NKEY], kstart[NKEY];
   const int t = threadIdx.x;
   const int chunk = (B + BUCKET_T - 1) / BUCKET_T;
   const int lo = min(B, t * chunk), hi = min(B, lo + chunk);
-  int c[NKEY];
-#pragma unroll
-  for (int k = 0; k < NKEY; ++k) c[k] = 0;
-  for (int q = lo; q < hi; ++q) {
-    const int key = min(max(need[q], 0), NKEY - 1);
-#pragma unroll
-    for (int k = 0; k < NKEY; ++k) c[k] += key == k;
-  }
-#pragma unroll
-  for (int k = 0; k < NKEY; ++k) s[k][t + 1] = c[k];
+  for (int k = 0; k < NKEY; ++k) s[k][t + 1] = 0;  // own column: no other thread touches it
   if (t < NKEY) s[t][0] = 0;
+  for (int q = lo; q < hi; ++q) s[min(max(need[q], 0), NKEY - 1)][t + 1] += 1;
   __syncthreads();
-  // exclusive scan over threads: wavefront w scans keys w, w + BUCKET_T / 64, ...
+  // inclusive scan of s[k][1 ..] over threads: wavefront w scans keys w, w + BUCKET_T / 64, ...
   for (int k = t / 64; k < NKEY; k += BUCKET_T / 64) {
     const int l = t % 64;
     int run = 0;
-    for (int base = 0; base < BUCKET_T; base += 64) {  // inclusive prefix of s[k][1 ..] in 64-wide tiles
+    for (int base = 0; base < BUCKET_T; base += 64) {
       int v = s[k][base + l + 1];
       for (int off = 1; off < 64; off <<= 1) {
         const int u = __shfl_up(v, off);
@@ -466,19 +469,16 @@ __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int
     if (l == 0) tot[k] = run;
   }
   __syncthreads();
-  int off[NKEY], start = 0;
-#pragma unroll
-  for (int k = 0; k < NKEY; ++k) {
-    off[k] = start + s[k][t];
-    start += tot[k];
+  if (t == 0) {
+    int st = 0;
+    for (int k = 0; k < NKEY; ++k) { kstart[k] = st; st += tot[k]; }
   }
+  __syncthreads();
+  // s[k][t] is now the number of key-k ids in the chunks before thread t's: stable scatter
   for (int q = lo; q < hi; ++q) {
     const int key = min(max(need[q], 0), NKEY - 1);
-    int pos = 0;
-#pragma unroll
-    for (int k = 0; k < NKEY; ++k)
-      if (key == k) pos = off[k]++;
-    list[pos] = q;
+    list[kstart[key] + s[key][t]] = q;
+    s[key][t] += 1;
   }
   if (t == 0) {
     int st = 0;
@@ -547,6 +547,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       const int q = atomicAdd(a.qhead + CLS, 1);
       L.sid[ls] = q < cnt ? a.slist[first + q] : -2;  // -2: queue drained, slot retires
       L.done[ls] = 0;
+      L.wmx[ls] = 0;
     }
     __syncthreads();
     const int slot_sc = lane < NT ? L.sid[ls] : -2;
@@ -624,6 +625,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     }
     wc.slot += wave_max(it_lane);
     ++wc.pass;
+    if (active) atomicMax(&L.wmx[ls], it_lane);
     __syncthreads();
     if (active) {
       ++iter;
@@ -702,6 +704,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         a.qstatus[(size_t)sc * n + i] = qstat;
         if (i == 0) {
           a.iters[sc] = iter;
+          a.ipmx[sc] = L.wmx[ls];
           L.sid[ls] = -1;
         }
       }
@@ -927,7 +930,7 @@ __host__ __device__ constexpr int dd_area_doubles(bool env) { return env ? ENV_L
 // sorted by k_bucket into one queue (class 0).
 __global__ void k_dd_key(KArgs a) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sc < a.B) a.need[sc] = NIB - 1 - iter_bin(a.iters[sc]);
+  if (sc < a.B) a.need[sc] = NIB - 1 - NPB * iter_bin(a.iters[sc]);
 }
 
 // DD control step (control/rqp_dd.py:695-752), persistent: each 64-lane block holds G = floor(64/n)
@@ -1560,7 +1563,7 @@ struct dat_handle {
   double *mind = nullptr, *err = nullptr;
   unsigned char* col = nullptr;
   unsigned long long* counters = nullptr;  // DAT_NCOUNTERS: [CNT_STRIDE k + .] of env class k (C-ADMM); [0..2] otherwise
-  int *need = nullptr, *slist = nullptr, *scount = nullptr;
+  int *need = nullptr, *slist = nullptr, *scount = nullptr, *ipmx = nullptr;
   double* erows = nullptr;     // C-ADMM: env rows of the step, k_env_class -> k_cadmm
   unsigned* emask = nullptr;
   long long hl_steps = 0;
@@ -1645,6 +1648,7 @@ KArgs kargs(dat_handle* h) {
   a.err = h->err;
   a.counters = h->counters;
   a.need = h->need;
+  a.ipmx = h->ipmx;
   a.erows = h->erows;
   a.emask = h->emask;
   a.slist = h->slist;
@@ -1789,6 +1793,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   if (c.record_err) rc |= dalloc(h, &h->err, B * (c.max_iter + 1));
   if (c.mode == DAT_MODE_CADMM) {
     rc |= dalloc(h, &h->need, B);
+    rc |= dalloc(h, &h->ipmx, B);
     rc |= dalloc(h, &h->erows, (size_t)B * n * DAT_NENV * 4);
     rc |= dalloc(h, &h->emask, (size_t)B * n);
     rc |= dalloc(h, &h->slist, B);
