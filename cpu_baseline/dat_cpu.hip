@@ -72,9 +72,11 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
   const int max_iter = 100;
   double rho = rho0;
   int it = 0;
+  const int prev_it = c.iters[sc];  // the previous step's ADMM iterations
   for (;;) {
     for (int i = 0; i < n; ++i) {
       lane_cadmm_dynamic(P[i], prm, n, i, Rt_all, lam + i * N3, fb, rho);
+      P[i].tuned = it == 0 || prev_it <= 3;  // as k_cadmm (tuned IPM start: first pass / warm regime)
       double y[1][3], w[6], best[best_size(1)];
       IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(rows_needed(P[i].emask), PlainRef<QPShared>{&S}, EnvPlain{&E[i]},
                                                RtPtr{Rt_all + 9 * i}, P[i], feq + 3 * i, y, w, best, 50, 1e-10);

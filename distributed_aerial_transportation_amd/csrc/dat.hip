@@ -538,7 +538,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   double* cfs = nullptr;  // the scenario's n agent copies f^(j), in the warm-state array (HBM / L2)
   double* myf = nullptr;
   double* bst = nullptr;
-  int iter = 0, qstat = ST_OPTIMAL;
+  int iter = 0, prev_iter = 0, qstat = ST_OPTIMAL;
   double rho = a.rho0;
   WaveCounters wc;
   for (;;) {
@@ -563,6 +563,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       myf = cfs + i * N3;
       bst = a.best + ((size_t)sc * n + i) * best_size(1);
       iter = 0;
+      prev_iter = a.iters[sc];  // the previous step's ADMM iterations (rewritten when the scenario stops)
       qstat = ST_OPTIMAL;
       rho = a.rho0;
       if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
@@ -593,6 +594,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     int it_lane = 0;
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
+      P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
       double y[1][3], w[6];
       IPMOut o;
       if constexpr (CLS >= ROWLDS_MIN_CLS && CLS < NCLS - 1) {

@@ -162,6 +162,7 @@ struct QPLane {
   int var;                       // C / cu variant
   unsigned emask;                // active env slots (compacted: bits 0 .. k-1)
   int infeasible;
+  int tuned;                     // C-ADMM: first ADMM pass of the step (tuned IPM start, see ipm_solve)
   double kappa, rho, min_fz, max_f, sec;
   double q[NB][3];               // per-block linear term
   double atil[6];                // C-ADMM: sum_{j != i} U_j a_j
@@ -318,6 +319,7 @@ DAT_HD void lane_common(QPLane<NB>& P, const double* prm) {
   P.sec = prm[DAT_P_SEC];
   P.emask = 0u;
   P.infeasible = 0;
+  P.tuned = 0;
 #pragma unroll
   for (int r = 0; r < 6; ++r) { P.atil[r] = 0.0; P.cw[r] = 0.0; }
   P.rho = 1.0;
@@ -656,14 +658,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   };
 
   // ---------------- initial point
-  // C-ADMM agent QPs: the tuned start and step fraction; DD agent QPs and the centralized QP (also
-  // the rigid payload on the same kernel, whose Jl^-1 ~ 50 grades the Newton systems): the
-  // conservative ones (on DD the tuned start lowers the mean IPM count but widens its spread over a
-  // wavefront: C3 29 -> 39 ms per step)
-  constexpr bool TUNED = MODE == MODE_CADMM;
-  constexpr double S0 = TUNED ? DAT_IPM_S0 : 1.0;
-  constexpr double Z0 = TUNED ? DAT_IPM_Z0 : 1.0;
-  constexpr double ETA = TUNED ? DAT_IPM_ETA : 0.99;
+  // The tuned start and step fraction for the C-ADMM agent QPs of a step's first ADMM pass and of
+  // scenarios whose previous step took <= 3 passes (P.tuned: the warm closed loop, whose multipliers
+  // are O(1e-2)); the conservative ones for the later passes of long ADMM runs (C2 / C5, cold random
+  // inputs and 17-28 passes: the tuned start everywhere took C2 13 -> 20 ms and C5 81 -> 118 ms per
+  // step), DD agent QPs (C3 29 -> 39 ms) and the centralized QP (also the rigid payload on the same
+  // kernel, whose Jl^-1 ~ 50 grades the Newton systems)
+  const bool TUNED = MODE == MODE_CADMM && P.tuned;
+  const double S0 = TUNED ? DAT_IPM_S0 : 1.0;
+  const double Z0 = TUNED ? DAT_IPM_Z0 : 1.0;
+  const double ETA = TUNED ? DAT_IPM_ETA : 0.99;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
 #pragma unroll
