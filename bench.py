@@ -7,6 +7,8 @@ every scenario, fully on device: forest desired-acceleration law + C-ADMM contro
 rows, up to 101 ADMM iterations of n agent QPs each) + 10 simulation steps (SO(3) PD + dynamics).
 
     python bench.py [--gpus N --steps K --warmup W --batch B --n 6 --mode cadmm]
+    python bench.py --gpus N --total-batch 65536   (strong scaling: BASELINE configs[3], 65,536 scenarios
+                                                   split over the N GPUs; the default is weak scaling)
     python bench.py --config C2|C3|C5 [--fixed-work]   (QP-level configs of SURVEY.md 8(d))
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
@@ -61,6 +63,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=None, help="scenarios per GPU (C4: 65536)")
+    ap.add_argument("--total-batch", type=int, default=None,
+                    help="strong scaling: this many scenarios in total, split over the ranks (BASELINE configs[3]: "
+                         "65536 across 8 GPUs = 8192 per GPU); the same global scenario set for every N")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--mode", default=None)
     ap.add_argument("--forests", type=int, default=64)
@@ -131,51 +136,66 @@ def cpu_baseline_qp(cfg: str, n: int, mode: str, budget_s: float, fixed_work: bo
                       f"{solves} agent QPs in {dt:.1f} s"}
 
 
-def cpu_baseline(n: int, budget_s: float, start: str = "path", forests_n: int = 64):
+def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: int, steps: int, batch: int):
     """The C4 closed loop on this host's cores (cpu_baseline/: the same per-scenario C-ADMM loop and
-    per-lane fp64 code as the GPU, OpenMP over scenarios, -O3 x86-64-v3) on a bounded sample of the
-    same workload: rank 0's start states, 2 untimed warm-up HL steps, then timed HL steps (desired
-    acceleration + C-ADMM control + 10 simulation steps) until the time budget is spent; once on
-    all OpenMP threads (the reported value) and once on 1 thread."""
+    per-lane fp64 code as the GPU, OpenMP over scenarios, -O3 x86-64-v3), work-matched to the GPU
+    line: the first S of rank 0's scenarios -- the same start states, forests and controller -- run
+    the bench's `warmup` untimed HL steps and then exactly its `steps` timed HL steps (desired
+    acceleration + C-ADMM control + 10 simulation steps), so the CPU solves the same agent QPs from the
+    same warm states as the GPU's timed region (S = all of them unless that exceeds ~budget_s; a
+    1-step calibration on a small subset sizes S).  Once on all OpenMP threads of this process (the
+    reported value) and once on 1 thread (the first 64 scenarios)."""
     import cpu_baseline as cb
     from distributed_aerial_transportation_amd import Forest, scenarios
 
     cb.build()
     threads = cb.CpuClosedLoop.max_threads()
-    S = max(256, 64 * threads)
-    scen_forest, seed = shard(0, S, forests_n)
-    rng = np.random.default_rng(seed)
-    forests = [Forest.seeded(s) for s in range(forests_n)]
-    if start == "path":
-        states = scenarios.forest_path_states(n, S, rng, forests, scen_forest)
-    else:
-        states = scenarios.forest_start_states(n, S, rng)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count()
+    scen_forest, states, forests = bench_states(n, batch, 0, 1, forests_n, start, None)
+    params = scenarios.params_block(n)
 
-    def run(nthreads, count, budget):
-        c = cb.CpuClosedLoop(n, S, scenarios.params_block(n))
-        c.set_forests(forests, scen_forest)
-        c.set_state(states)
-        c.closed_loop(2, count=count, threads=nthreads)  # warm-up: the GPU bench times warm steps too
-        q = ipm = steps = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < budget:
-            dq, di = c.closed_loop(1, count=count, threads=nthreads)
-            q, ipm, steps = q + dq, ipm + di, steps + 1
-        return q / (time.perf_counter() - t0), q, ipm, steps
+    def ctx(count):
+        c = cb.CpuClosedLoop(n, count, params)
+        c.set_forests(forests, scen_forest[:count])
+        c.set_state(states[:count])
+        return c
 
-    v1, q1, _, st1 = run(1, min(S, 64), 0.25 * budget_s)
-    vN, qN, iN, stN = run(threads, S, 0.75 * budget_s)
+    # calibration: one HL step of a small subset from the start states (scenario-steps per second)
+    S0 = min(batch, 32 * threads)
+    cal = ctx(S0)
+    t0 = time.perf_counter()
+    cal.closed_loop(1, threads=threads)
+    rate = S0 / max(time.perf_counter() - t0, 1e-6)
+    cal.close()
+    S = int(min(batch, max(S0, budget_s * rate / max(steps, 1))))
+    c = ctx(S)
+    c.closed_loop(warmup, threads=threads)  # the GPU line's untimed warm-up steps
+    t0 = time.perf_counter()
+    qN, iN = c.closed_loop(steps, threads=threads)
+    tN = time.perf_counter() - t0
+    c.close()
+    S1 = min(S, 64)
+    c1 = ctx(S1)
+    c1.closed_loop(warmup, threads=1)
+    t0 = time.perf_counter()
+    q1, _ = c1.closed_loop(steps, threads=1)
+    t1 = time.perf_counter() - t0
+    c1.close()
     try:
         cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except (OSError, IndexError):
         cpu = "unknown"
-    return {"value": vN, "unit": "agent-QP solves/s", "cores": threads, "kind": "port",
-            "single_core_value": v1,
+    return {"value": qN / tN, "unit": "agent-QP solves/s", "cores": threads, "affinity_cpus": affinity,
+            "kind": "port", "single_core_value": q1 / t1, "ipm_iters_per_qp": iN / max(qN, 1),
             "sample": f"C++ OpenMP restatement of the C4 loop (cpu_baseline/dat_cpu.hip, same per-lane code as the "
-                      f"kernels), n={n}, {S} of the bench's {start}-start scenarios, {stN} warm HL steps "
-                      f"({qN} agent QPs, {iN / max(qN, 1):.2f} IPM it/QP) on {threads} threads; 1 thread: "
-                      f"{min(S, 64)} scenarios x {st1} steps ({q1} QPs); host CPU {cpu}, os.cpu_count() "
-                      f"{os.cpu_count()}"}
+                      f"kernels), n={n}: the first {S} of the bench's {batch} {start}-start scenarios (rank 0), "
+                      f"{warmup} untimed + {steps} timed HL steps like the GPU line ({qN} agent QPs, "
+                      f"{iN / max(qN, 1):.2f} IPM it/QP, {tN:.1f} s) on {threads} OpenMP threads (the box's CPU "
+                      f"share; sched_getaffinity: {affinity} CPUs); 1 thread: {S1} scenarios x {steps} steps "
+                      f"({q1} QPs); host CPU {cpu}, os.cpu_count() {os.cpu_count()}"}
 
 
 def shard(rank: int, batch: int, num_forests: int):
@@ -183,6 +203,38 @@ def shard(rank: int, batch: int, num_forests: int):
     s drives forest s mod num_forests; start states from a per-rank seed."""
     ids = np.arange(batch) + rank * batch
     return ids % num_forests, 1000 + rank
+
+
+def strong_shard(rank: int, world: int, total: int):
+    """Strong scaling: contiguous split of `total` scenario ids over `world` ranks (the first
+    total % world ranks take one more)."""
+    base, extra = divmod(total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, base + (1 if rank < extra else 0)
+
+
+def bench_states(n: int, batch: int, rank: int, world: int, forests_n: int, start: str, total):
+    """(scenario_forest, start states, forests) of one rank.  Weak scaling (total None): `batch`
+    scenarios from the per-rank seed (shard).  Strong scaling: the global set of `total` scenarios from
+    one seed, every rank taking its contiguous slice (strong_shard), so every N runs the same scenarios."""
+    from distributed_aerial_transportation_amd import Forest, scenarios
+
+    forests = [Forest.seeded(s) for s in range(forests_n)]
+    if total is None:
+        sf, seed = shard(rank, batch, forests_n)
+        ids, count = None, batch
+    else:
+        lo, cnt = strong_shard(rank, world, total)
+        sf, seed = shard(0, total, forests_n)
+        ids, count = slice(lo, lo + cnt), total
+    rng = np.random.default_rng(seed)
+    if start == "path":
+        st = scenarios.forest_path_states(n, count, rng, forests, sf)
+    else:
+        st = scenarios.forest_start_states(n, count, rng)
+    if ids is not None:
+        sf, st = sf[ids], st[ids]
+    return np.ascontiguousarray(sf), np.ascontiguousarray(st), forests
 
 
 def combine_ranks(dist, world: int, tot: np.ndarray, metrics: np.ndarray, device):
@@ -303,19 +355,15 @@ def main():
         if args.selftest:
             sys.exit("bench.py: --selftest covers the C4 path only")
         return qp_level(args, dist, rank, world, local)
-    n, B = args.n, args.batch
-    scen_forest, seed = shard(rank, B, args.forests)
-    rng = np.random.default_rng(seed)
+    n = args.n
+    total = args.total_batch
+    B = args.batch if total is None else strong_shard(rank, world, total)[1]
     if args.selftest:
         eng = _SelftestEngine(n, B, rank)
     else:
-        from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+        from distributed_aerial_transportation_amd import BatchedController, scenarios
 
-        forests = [Forest.seeded(s) for s in range(args.forests)]
-        if args.start == "path":
-            states = scenarios.forest_path_states(n, B, rng, forests, scen_forest)
-        else:
-            states = scenarios.forest_start_states(n, B, rng)
+        scen_forest, states, forests = bench_states(n, B, rank, world, args.forests, args.start, total)
         eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
         eng.set_forests(forests, scen_forest)
         eng.set_state(states, np.zeros(B, dtype=np.int32))
@@ -337,15 +385,18 @@ def main():
     # per-scenario metrics of the last step (all-gathered over ranks: the only collective)
     res = eng.control(None, None)
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
-    tot = np.array([qps, ipm, hl_ms, elapsed, row_it], dtype=np.float64)
+    tot = np.array([qps, ipm, hl_ms, elapsed, row_it, work.get("inband_exits", 0), B,
+                    work.get("inband_beyond_clarabel_tol", 0)], dtype=np.float64)
     if dist is not None:
         sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, dev)
         qps_all, ipm_all, row_all = float(sums[0]), float(sums[1]), float(sums[4])
+        inband_all, scen_all, loose_all = int(sums[5]), int(sums[6]), int(sums[7])
         elapsed = float(maxs[3])
         hl_ms_rank0 = float(tot[2])
     else:
         all_metrics = local_metrics
         qps_all, ipm_all, row_all, hl_ms_rank0 = float(qps), float(ipm), float(row_it), float(hl_ms)
+        inband_all, scen_all, loose_all = int(tot[5]), B, int(tot[7])
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -371,7 +422,11 @@ def main():
     kernel_ms = k_ms / max(hl_steps, 1)
     flops_launch = (FLOPS_FIXED * k_ipm + FLOPS_PER_ROW * k_row) / max(hl_steps, 1)
     achieved_tflops = flops_launch / max(kernel_ms * 1e-3, 1e-12) / 1e12
-    workload = f"C4: {args.mode} n={n}, forest env ({args.start} start), {B} closed-loop scenarios per GPU"
+    if total is None:
+        workload = f"C4: {args.mode} n={n}, forest env ({args.start} start), {B} closed-loop scenarios per GPU"
+    else:
+        workload = (f"C4: {args.mode} n={n}, forest env ({args.start} start), {total} closed-loop scenarios split "
+                    f"over {world} GPU(s)")
     traffic, traffic_src = traffic_per_launch(kernel, workload)
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
@@ -384,17 +439,21 @@ def main():
         "ms_per_step_p50": float(np.percentile(per_step, 50)),
         "ms_per_step_p99": float(np.percentile(per_step, 99)),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if total is None else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": ("selftest (no solver work; synthetic counters)" if args.selftest else
                  f"synthetic (seeded forests 0..63, randomized C4 {args.start} start states)"),
         "config": {"workload": workload,
-                   "n": n, "scenarios_per_gpu": B, "hl_every": 10, "dt": 1e-3, "parallelism": f"scenario-sharded x{world}"},
+                   "n": n, "scenarios_per_gpu": B, "total_scenarios": scen_all, "hl_every": 10, "dt": 1e-3,
+                   "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
                   "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
-                  "hl_kernel_ms_per_step": launch_ms, "env_classes": classes},
+                  "hl_kernel_ms_per_step": launch_ms, "env_classes": classes,
+                  # agent QPs accepted through the best in-band iterate, and those beyond Clarabel's
+                  # 1e-8 tolerance (dat_get_inband_exits)
+                  "inband_exits": inband_all, "inband_beyond_clarabel_tol": loose_all},
         "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "kernel": kernel, "launch_ms": kernel_ms,
@@ -402,7 +461,7 @@ def main():
                      "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"},
     }
     if not args.no_cpu_baseline and world == 1 and not args.selftest:
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start)
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start, args.forests, args.warmup, args.steps, B)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -488,7 +547,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
                   "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
-                  "kernel_ms_per_step": step_ms},
+                  "kernel_ms_per_step": step_ms, "inband_exits": int(w.get("inband_exits", 0)),
+                  "inband_beyond_clarabel_tol": int(w.get("inband_beyond_clarabel_tol", 0))},
         "roofline": {"bound": "fp64-valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kernel, "launch_ms": launch_ms,
                      "flops_per_launch": flops_launch,

@@ -59,7 +59,8 @@ def lib():
         L.datcpu_set_forests.argtypes = [ctypes.c_void_p, ctypes.c_int, I, D, I, D]
         L.datcpu_set_state.argtypes = [ctypes.c_void_p, D]
         L.datcpu_closed_loop.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                         ctypes.c_double, LL, LL]
+                                         ctypes.c_int, ctypes.c_double, LL, LL]
+        L.datcpu_reset_warm.argtypes = [ctypes.c_void_p]
         L.datcpu_get.argtypes = [ctypes.c_void_p, D, D, I]
         _lib = L
     return _lib
@@ -110,10 +111,16 @@ class CpuClosedLoop:
         st = np.ascontiguousarray(states, dtype=np.float64)
         assert lib().datcpu_set_state(self._h, _p(st)) == 0
 
-    def closed_loop(self, hl_steps: int, count: int = None, threads: int = 0, hl_every: int = 10, dt: float = 1e-3):
+    def reset_warm(self) -> None:
+        """The constructor's warm state and no step history (dat_reset_warm_start on the GPU)."""
+        assert lib().datcpu_reset_warm(self._h) == 0
+
+    def closed_loop(self, hl_steps: int, count: int = None, threads: int = 0, hl_every: int = 10, dt: float = 1e-3,
+                    first: int = 0):
+        """hl_steps closed-loop periods of scenarios [first, first + count); (agent QPs, IPM iterations)."""
         q, it = ctypes.c_longlong(), ctypes.c_longlong()
-        count = self.batch if count is None else count
-        assert lib().datcpu_closed_loop(self._h, hl_steps, count, threads, hl_every, dt, ctypes.byref(q),
+        count = self.batch - first if count is None else count
+        assert lib().datcpu_closed_loop(self._h, hl_steps, first, count, threads, hl_every, dt, ctypes.byref(q),
                                         ctypes.byref(it)) == 0
         return q.value, it.value
 

@@ -172,16 +172,33 @@ int datcpu_set_state(void* h, const double* state) {
   return 0;
 }
 
-// hl_steps closed-loop periods of scenarios [0, count) on `threads` OpenMP threads (0: default);
-// returns the agent-QP solves and IPM iterations of the call.
-int datcpu_closed_loop(void* h, int hl_steps, int count, int threads, int hl_every, double dt, long long* qp_solves,
-                       long long* ipm_iters) {
+// the constructor's warm state (f = f_mean = f_eq, lambda = 0, control/rqp_cadmm.py:577-580) and no
+// step history (the previous step's ADMM iteration count selects the IPM start, as on the GPU: k_warm)
+int datcpu_reset_warm(void* h) {
   Ctx* c = (Ctx*)h;
-  if (!c || count < 0 || count > c->B) return -1;
+  if (!c) return -1;
+  const size_t N3 = 3 * (size_t)c->n;
+  const double* feq = c->params.data() + DAT_P_FEQ(c->n);
+  std::fill(c->clam.begin(), c->clam.end(), 0.0);
+  std::fill(c->iters.begin(), c->iters.end(), 0);
+  for (int b = 0; b < c->B; ++b) {
+    for (int i = 0; i < c->n; ++i) std::memcpy(&c->cf[((size_t)b * c->n + i) * N3], feq, sizeof(double) * N3);
+    std::memcpy(&c->cfbar[(size_t)b * N3], feq, sizeof(double) * N3);
+    std::memcpy(&c->fdes[(size_t)b * N3], feq, sizeof(double) * N3);
+  }
+  return 0;
+}
+
+// hl_steps closed-loop periods of scenarios [first, first + count) on `threads` OpenMP threads (0:
+// default); returns the agent-QP solves and IPM iterations of the call.
+int datcpu_closed_loop(void* h, int hl_steps, int first, int count, int threads, int hl_every, double dt,
+                       long long* qp_solves, long long* ipm_iters) {
+  Ctx* c = (Ctx*)h;
+  if (!c || first < 0 || count < 0 || first + count > c->B) return -1;
   long long qp = 0, ipm = 0;
   if (threads <= 0) threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads) reduction(+ : qp, ipm)
-  for (int sc = 0; sc < count; ++sc) {
+  for (int sc = first; sc < first + count; ++sc) {
     for (int k = 0; k < hl_steps; ++k) {
       cadmm_step(*c, sc, &qp, &ipm);
       double* st = c->state.data() + (size_t)sc * c->S;

@@ -114,6 +114,8 @@ EXPORTS = {
     "dat_solve_agent_qp_batch": (ctypes.c_int, [H, ctypes.c_int, I, I, D, D, D, D, D, D, I, I, U8, D]),
     "dat_set_low_level": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_get_kernel_ms": (ctypes.c_int, [H, D]),
+    "dat_get_inband_exits": (ctypes.c_int, [H, LL, LL]),
+    "dat_get_agent_qp_ms": (ctypes.c_int, [H, D]),
     "dat_rp_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_low_level_control": (ctypes.c_int, [H, D, D, D]),
 }

@@ -252,8 +252,16 @@ class BatchedController:
                              ctypes.c_double())
         L.check(self._lib.dat_get_counters(self._h, ctypes.byref(q), ctypes.byref(it), ctypes.byref(rw),
                                            ctypes.byref(hs), ctypes.byref(ms)))
+        ib, lo = ctypes.c_longlong(), ctypes.c_longlong()
+        L.check(self._lib.dat_get_inband_exits(self._h, ctypes.byref(ib), ctypes.byref(lo)))
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
-                "hl_kernel_ms": ms.value}
+                "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value}
+
+    def agent_qp_ms(self) -> float:
+        """Device time of the last solve_agent_qps launch (dat_get_agent_qp_ms)."""
+        ms = ctypes.c_double()
+        L.check(self._lib.dat_get_agent_qp_ms(self._h, ctypes.byref(ms)))
+        return ms.value
 
     def class_work(self, env_class: int) -> dict:
         """C-ADMM only: work counters, summed kernel time and SIMD occupancy of one env class (0:
@@ -366,36 +374,42 @@ class _PrimalSolver:
     def _run(self, state, acc_des, **kw):
         self._eng.set_state(pack_state(state)[None])
         acc = np.concatenate([np.asarray(acc_des[0], float), np.asarray(acc_des[1], float)])[None]
-        t0 = self._eng.work()["hl_kernel_ms"]
         r = self._eng.solve_agent_qps([0], [self.i], acc, **kw)
         self.collision, self.min_env_dist = bool(r["collision"][0]), float(r["min_env_dist"][0])
         if self.verbose and r["status"][0] != L.QP_OPTIMAL:
             print(f"Problem not solved to optimality, status: {int(r['status'][0])}")
-        return r, t0
+        # solve_time [s]: the device time of the QP kernel, as Clarabel's solver_stats.solve_time is the
+        # solver's own time (control/rqp_cadmm.py:500)
+        return r, self._eng.agent_qp_ms() * 1e-3
 
 
 class RQPCADMMPrimalSolver(_PrimalSolver):
     """control/rqp_cadmm.py:26-507: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) ->
     (f (3, n), solve_time, collision, min_env_dist).  Exception -> f_eq (:491-494); non-OPTIMAL ->
-    previous solution (:496-499).  cadmm_rho must be > 0 (at rho = 0 -- the constructor's warm-up solve,
-    :131-140 -- the copies f_j, j != i, are not unique; that solve only seeds Clarabel's warm start)."""
+    previous solution (:496-499).  cadmm_rho must be > 0: the reference's default 0 (:487) is its
+    constructor's warm-up solve (:131-140), at which the copies f_j, j != i, are not unique (that solve
+    only seeds Clarabel's warm start); rho <= 0 raises ValueError instead of silently solving another QP."""
 
     _mode = L.MODE_CADMM
 
     def _set_warm_start(self) -> None:
         self.prev_f = self.f_eq.copy()
 
-    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 1.0, f_mean=None):
+    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 0, f_mean=None):
         n = self.n
+        if not float(cadmm_rho) > 0.0:
+            raise ValueError(f"cadmm_rho must be > 0 (got {cadmm_rho}): at rho = 0 the agent QP's copies f_j, "
+                             "j != i, are not unique (the reference uses rho = 0 only for its constructor's "
+                             "warm-up solve, control/rqp_cadmm.py:131-140)")
         lam = np.zeros((3, n)) if lambda_f is None else np.asarray(lambda_f, float)
         fm = np.zeros((3, n)) if f_mean is None else np.asarray(f_mean, float)
-        r, _ = self._run(state, acc_des, lam=lam[None], rho=[cadmm_rho], f_mean=fm[None])
+        r, t = self._run(state, acc_des, lam=lam[None], rho=[cadmm_rho], f_mean=fm[None])
         st = int(r["status"][0])
         if st == L.QP_FAILED:
             self.prev_f = self.f_eq.copy()
         elif st == L.QP_OPTIMAL:
             self.prev_f = r["x"][0].copy()
-        return self.prev_f, 0.0, self.collision, self.min_env_dist
+        return self.prev_f, t, self.collision, self.min_env_dist
 
 
 class RQPDDPrimalSolver(_PrimalSolver):
@@ -413,14 +427,14 @@ class RQPDDPrimalSolver(_PrimalSolver):
 
     def solve(self, state, acc_des, c_fi=np.zeros(3), c_Fi=np.zeros(3), c_Mi=np.zeros(3)):
         c = np.concatenate([np.asarray(c_fi, float), np.asarray(c_Fi, float), np.asarray(c_Mi, float)])
-        r, _ = self._run(state, acc_des, c=c[None])
+        r, t = self._run(state, acc_des, c=c[None])
         st = int(r["status"][0])
         if st == L.QP_FAILED:
             self._set_warm_start()
         elif st == L.QP_OPTIMAL:
             x = r["x"][0]
             self.prev_fi, self.prev_Fi, self.prev_Mi = x[:3].copy(), x[3:6].copy(), x[6:].copy()
-        return self.prev_fi, self.prev_Fi, self.prev_Mi, 0.0, self.collision, self.min_env_dist
+        return self.prev_fi, self.prev_Fi, self.prev_Mi, t, self.collision, self.min_env_dist
 
 
 class RQPLowLevelController:

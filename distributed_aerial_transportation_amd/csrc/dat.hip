@@ -66,7 +66,12 @@ __host__ __device__ inline int iter_bin(int it) {
 __host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
 constexpr int NKEY = NCLS * NIB;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
-constexpr int DAT_NCOUNTERS = NCLS * CNT_STRIDE;
+// QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
+// scaled residual / gap exceeds Clarabel's own tolerance (INBAND_CLARABEL)
+constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
+constexpr int DAT_NCOUNTERS = CNT_INBAND + 2;
+constexpr double INBAND_CLARABEL = 1e-8;
+__device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
 
 struct KArgs {
   int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)
@@ -136,7 +141,8 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
 //                 <= 10), collision, min env distance, and a sort key (class, previous step's
 //                 ADMM iteration count); the rows go to HBM (erows / emask, SoA over agents) and
 //                 k_cadmm loads them when a slot takes the scenario instead of re-running the query;
-//   k_bucket      stable counting sort of the scenario ids by key (one queue per class);
+//   k_bucket      counting sort of the scenario ids by key (one queue per class; the order within a
+//                 key is not fixed, see k_bucket);
 //   k_cadmm       persistent blocks (CUs x 4) drain the class queues, classes 3, 2, 1, 0 in turn,
 //                 each with its own row-slot instantiation of the IPM (3 + {10, 5, 2, 0} slots:
 //                 the register footprint follows the rows the class needs); a scenario slot that
@@ -444,6 +450,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // scenarios share a wavefront, never a scenario's arithmetic (the capped-grid test compares two
 // different groupings bitwise).
 constexpr int BUCKET_T = 1024;
+static_assert(NKEY <= BUCKET_T, "k_bucket initialises one key per thread");
 __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int* list, int* count) {
   __shared__ int hist[NKEY], kstart[NKEY], cursor[NKEY], tot[NKEY];
   const int t = threadIdx.x;
@@ -476,6 +483,7 @@ __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int
 // Work counters of one wavefront, flushed once per class it drained.
 struct WaveCounters {
   long long qp = 0, ipm = 0, rowit = 0;  // lane-level: agent-QP solves, IPM iterations, x active rows
+  long long inband = 0, loose = 0;      // lane-level: solves accepted through the best in-band iterate
   long long slot = 0, pass = 0;         // wave-level: sum of (max lane IPM iterations) per pass, passes
 };
 
@@ -589,6 +597,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
                                          IPM_TOL);
       }
       wc.ipm += o.iters;
+      wc.inband += o.inband;
+      wc.loose += inband_loose(o);
       it_lane = o.iters;
       wc.rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++wc.qp;
@@ -695,10 +705,13 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   }
   // work counters of this class: one atomic per wavefront
   unsigned long long q = (unsigned long long)wc.qp, ip = (unsigned long long)wc.ipm, rw = (unsigned long long)wc.rowit;
+  unsigned long long ib = (unsigned long long)wc.inband, lo = (unsigned long long)wc.loose;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
     rw += __shfl_xor(rw, off);
+    ib += __shfl_xor(ib, off);
+    lo += __shfl_xor(lo, off);
   }
   if (lane == 0) {
     unsigned long long* cc = a.counters + CNT_STRIDE * CLS;
@@ -707,6 +720,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     atomicAdd(cc + 2, rw);
     atomicAdd(cc + 3, (unsigned long long)(wc.slot * NT));
     atomicAdd(cc + 4, (unsigned long long)(wc.pass * G));
+    if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
+    if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
   }
   __syncthreads();
 }
@@ -716,7 +731,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
 // instantiation of the IPM.  All wavefronts work on the same class at (nearly) the same time: the
 // unrolled IPM of one class is ~80-130 KB of code, and wavefronts of different classes sharing a
 // CU's instruction cache measured 16 % slower (proportional class starts: 12.9 vs 11.1 ms, C4 path).
-__global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
+#ifdef DAT_CADMM_WPE  // development knob: register budget of k_cadmm (waves per SIMD)
+#define DAT_CADMM_ATTR __attribute__((amdgpu_waves_per_eu(DAT_CADMM_WPE)))
+#else
+#define DAT_CADMM_ATTR
+#endif
+__global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm(KArgs a) {
   cadmm_drain<3>(a);
   cadmm_drain<2>(a);
   cadmm_drain<1>(a);
@@ -958,7 +978,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double prev[9];
   int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
   double mdist = 0.0;
-  long long my_ipm = 0, my_qp = 0, my_rowit = 0;
+  long long my_ipm = 0, my_qp = 0, my_rowit = 0, my_inband = 0, my_loose = 0;
   for (;;) {
     // ---- refill empty slots from the queue
     if (lane < NT && i == 0 && sid[ls] == -1) {
@@ -1031,6 +1051,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                          IPM_TOL);
       my_ipm += o.iters;
+      my_inband += o.inband;
+      my_loose += inband_loose(o);
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
@@ -1128,15 +1150,20 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     __syncthreads();
   }
   unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
+  unsigned long long ib = (unsigned long long)my_inband, lo = (unsigned long long)my_loose;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
     rw += __shfl_xor(rw, off);
+    ib += __shfl_xor(ib, off);
+    lo += __shfl_xor(lo, off);
   }
   if (lane == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
     atomicAdd(a.counters + 2, rw);
+    if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
+    if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
   }
 }
 
@@ -1148,7 +1175,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = sc < a.B;
   const int n = NB;
-  unsigned long long q = 0, ip = 0, rw = 0;
+  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0;
   const double* prm = valid ? prm_of(a, sc) : a.params;
   QPShared S;
   QPLane<NB> P;
@@ -1179,6 +1206,8 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
                                              IPM_MAX_ITER, IPM_TOL);
     q = 1;
     ip = o.iters;
+    ib = o.inband;
+    lo = inband_loose(o);
     rw = (unsigned long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
     double* pf = a.pf + (size_t)sc * 3 * n;
     if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
@@ -1194,11 +1223,15 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
     rw += __shfl_xor(rw, off);
+    ib += __shfl_xor(ib, off);
+    lo += __shfl_xor(lo, off);
   }
   if (threadIdx.x == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
     atomicAdd(a.counters + 2, rw);
+    if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
+    if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
   }
 }
 
@@ -1393,6 +1426,10 @@ __global__ void k_warm(KArgs a) {
   if (a.pf)
     for (int c = 0; c < N3; ++c) a.pf[(size_t)sc * N3 + c] = feq[c];
   for (int c = 0; c < N3; ++c) a.fdes[(size_t)sc * N3 + c] = feq[c];
+  // the previous step's ADMM / DD iteration count and slowest IPM count select the IPM start (C-ADMM
+  // warm regime) and the drain order: a reset handle behaves exactly like a freshly created one
+  a.iters[sc] = 0;
+  if (a.ipmx) a.ipmx[sc] = 0;
 }
 
 __global__ void k_env(KArgs a, double* lhs, double* rhs, int* nrow, unsigned char* col, double* md) {
@@ -1550,6 +1587,7 @@ struct dat_handle {
   unsigned* emask = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
+  double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
 };
@@ -2163,8 +2201,10 @@ int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, cons
   hipError_t e = hipSuccess;
   if (ok) {
     KArgs a = kargs(h);
+    e = hipEventRecord(h->e0, h->stream);
     hipLaunchKernelGGL(k_agent_qp, dim3((count + 63) / 64), dim3(64), 0, h->stream, a, q);
-    e = hipGetLastError();
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(h->e1, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(x, q.x, sizeof(double) * C * nx, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(status, q.status, sizeof(int) * C, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && ipm_iters) e = hipMemcpyAsync(ipm_iters, q.iters, sizeof(int) * C, hipMemcpyDeviceToHost, h->stream);
@@ -2173,6 +2213,10 @@ int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, cons
       e = hipMemcpyAsync(min_env_dist, q.mind, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream);
   }
   hipError_t es = hipStreamSynchronize(h->stream);
+  if (ok && e == hipSuccess && es == hipSuccess) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->e0, h->e1) == hipSuccess) h->agent_qp_ms = ms;
+  }
   for (void* p : tmp) (void)hipFree(p);
   if (!ok) return fail("dat_solve_agent_qp_batch: device allocation failed");
   if (e != hipSuccess) return fail(std::string("dat_solve_agent_qp_batch: ") + hipGetErrorString(e));
@@ -2214,6 +2258,23 @@ int dat_low_level_control(dat_handle* h, const double* f_des, double* thrust, do
 int dat_get_kernel_ms(dat_handle* h, double* ms) {
   if (!h || !ms) return fail("dat_get_kernel_ms: null argument");
   *ms = h->cadmm_ms;
+  return 0;
+}
+
+int dat_get_agent_qp_ms(dat_handle* h, double* ms) {
+  if (!h || !ms) return fail("dat_get_agent_qp_ms: null argument");
+  *ms = h->agent_qp_ms;
+  return 0;
+}
+
+int dat_get_inband_exits(dat_handle* h, long long* inband, long long* beyond_clarabel_tol) {
+  if (!h) return fail("dat_get_inband_exits: null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_INBAND, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (inband) *inband = (long long)c[0];
+  if (beyond_clarabel_tol) *beyond_clarabel_tol = (long long)c[1];
   return 0;
 }
 

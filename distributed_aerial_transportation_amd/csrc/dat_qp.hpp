@@ -513,6 +513,10 @@ __host__ __device__ constexpr int row_lds_doubles(int NR) { return 3 * NR * 64; 
 struct IPMOut {
   int status;
   int iters;
+  int inband;     // OPTIMAL through the best in-band iterate of a stalled solve (not converged to tol)
+  double merit;   // scaled max(primal residual, dual residual, gap) of the returned iterate
+  int why;        // exit: 0 converged, 1 non-finite residuals, 2 divergence / max_iter, 3 cone scaling,
+                  // 4 cone block D, 5 Cholesky of M, 6 Cholesky of N
   double pi[6];   // u-space gradient C u + cu - A' z_rows at the solution
   double u[6];
 };
@@ -537,6 +541,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   IPMOut out;
   out.status = ST_FAILED;
   out.iters = 0;
+  out.inband = 0;
+  out.why = 0;
+  out.merit = 1e300;
 #pragma unroll
   for (int r = 0; r < 6; ++r) { out.pi[r] = 0.0; out.u[r] = 0.0; }
   if (sh.get().infeasible || P.infeasible) {
@@ -789,11 +796,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         // at the initial point: the problem data itself is not finite (the solver-exception
         // branch); later: a numerical breakdown of a finite problem (not solved)
         out.status = it == 0 ? ST_FAILED : ST_INACCURATE;
+        out.why = 1;
         break;
       }
       double merit = fmax(fmax(pres / nh, dres / nq), gap);
+#ifdef DAT_IPM_TRACE
+      printf("ipm it %2d pres %.3e dres %.3e gap %.3e merit %.3e\n", it, pres / nh, dres / nq, gap, merit);
+#endif
       if (pres < tol * nh && dres < tol * nq && gap < 10.0 * tol) {
         out.status = ST_OPTIMAL;
+        out.merit = merit;
 #pragma unroll
         for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
         return out;
@@ -818,6 +830,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
       best_merit = fmin(best_merit, merit);
       if ((it >= 4 && merit > DAT_IPM_DIVERGE * best_merit) || it >= max_iter) {
+        out.why = 2;
         break;
       }
       if (it >= max_iter) break;
@@ -835,7 +848,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       soc_apply(S1[k], zk[k] + 1, lamk[k] + 1, false);
       soc_apply(S2[k], zk[k] + 5, lamk[k] + 5, false);
     }
-    if (!okc) break;
+    if (!okc) {
+      out.why = 3;
+      break;
+    }
     auto winv = [&](int k, const double* v, double* o) {  // W_k^-1 v
       o[0] = v[0] * id0[k];
       soc_apply(S1[k], v + 1, o + 1, true);
@@ -874,7 +890,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         }
       okc = okc && inv3_spd(D, Dinv[k]);
     }
-    if (!okc) break;
+    if (!okc) {
+      out.why = 4;
+      break;
+    }
     // M = Lm Lm' (Cholesky; M is SPD: C carries k_f, k_m > 0) and, for CADMM / CENT, the Cholesky
     // factor Ln of the SPD matrix N = I + Lm' T Lm, so that (I + M T)^-1 M = Lm N^-1 Lm' =: P.  N has
     // every eigenvalue >= 1 however large active rows make M, so the factorisation stays well
@@ -922,9 +941,15 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           }
       }
       if (MODE == MODE_DD) {
-        if (!chol6(Mm, Lm)) break;
+        if (!chol6(Mm, Lm)) {
+          out.why = 5;
+          break;
+        }
       } else {
-        if (!chol6_lower(Mm, Lm)) break;
+        if (!chol6_lower(Mm, Lm)) {
+          out.why = 5;
+          break;
+        }
         // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho)
         double T[21];
         if (MODE == MODE_CADMM) {
@@ -942,7 +967,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         }
         double Nn[21], Ln[21];
         ltl_plus_identity(Lm, T, Nn);
-        if (!chol6(Nn, Ln)) break;
+        if (!chol6(Nn, Ln)) {
+          out.why = 6;
+          break;
+        }
         double Pm[21];
         schur_P(Lm, Ln, Pm);
 #pragma unroll
@@ -1300,6 +1328,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       out.u[r] = best[3 * NB + 12 + r];
     }
     out.status = ST_OPTIMAL;
+    out.inband = 1;
+    out.merit = best_key;
   }
   return out;
 }

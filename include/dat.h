@@ -153,6 +153,18 @@ int dat_set_persistent_blocks(dat_handle* h, int blocks);
  * k_cadmm (C-ADMM) or k_dd (DD; the per-scenario quasi-Newton setup k_dd_setup excluded), 0 for
  * centralized.  Both are persistent queue drains; dat_set_persistent_blocks caps their grid. */
 int dat_get_kernel_ms(dat_handle* h, double* ms);
+/* Agent QPs since the last counter reset (every kernel) that stalled before the IPM tolerance (1e-10:
+ * a numerical breakdown of the structured Newton solve at gaps ~1e-12, or the divergence stop) and
+ * were accepted as OPTIMAL through their best iterate inside north_star's band (scaled primal / dual
+ * residuals <= 1e-7, gap <= 1e-6); beyond_clarabel_tol counts those whose returned iterate is outside
+ * Clarabel's own stopping tolerance (1e-8: a point Clarabel would not yet report as solved).  The
+ * reference holds its previous solution on a non-OPTIMAL status (control/rqp_cadmm.py:496-499), so
+ * beyond_clarabel_tol bounds the branch-disagreement risk; the C-ADMM / DD parity tests require 0. */
+int dat_get_inband_exits(dat_handle* h, long long* inband, long long* beyond_clarabel_tol);
+/* Device time [ms] of the last dat_solve_agent_qp_batch launch (k_agent_qp; HIP events on the handle's
+ * stream): the solve_time RQPPrimalSolver.solve returns (Clarabel's solver_stats.solve_time,
+ * control/rqp_cadmm.py:500, control/rqp_dd.py:497). */
+int dat_get_agent_qp_ms(dat_handle* h, double* ms);
 
 /* ---- raw batched kernels (tests / benchmarking of single pieces) ---------------------------
  * dat_env_rows: _set_collision_avoidance_cbf_parameters (control/rqp_cadmm.py:307-373,

@@ -86,7 +86,16 @@ def capsule_tree_distance(x0, x1, radius, c):
     seg = x1 - x0
     f = lambda t: _point_cyl(x0 + t * seg, c)[0]
     ts = np.linspace(0.0, 1.0, 2001)
-    vals = np.array([f(t) for t in ts])
+    # the dense sample (vectorised _point_cyl) only brackets the minimiser; the refinement below and
+    # the returned points use the scalar path
+    P = x0[None, :] + ts[:, None] * seg[None, :]
+    dxy = P[:, :2] - c[:2]
+    rho = np.sqrt(dxy[:, 0] ** 2 + dxy[:, 1] ** 2)
+    Q = P.copy()
+    out = rho > BARK_RADIUS
+    Q[out, :2] = c[:2] + dxy[out] / rho[out, None] * BARK_RADIUS
+    Q[:, 2] = c[2] + np.clip(P[:, 2] - c[2], -BARK_HEIGHT / 2, BARK_HEIGHT / 2)
+    vals = np.sqrt(np.sum((P - Q) ** 2, axis=1))
     k = int(np.argmin(vals))
     lo, hi = ts[max(k - 1, 0)], ts[min(k + 1, len(ts) - 1)]
     if hi > lo:

@@ -367,7 +367,7 @@ def gen_rp():
              fd_s=np.array(fd_s), fd_f=np.array(fd_f), fd_acc=np.array(fd_acc))
 
 
-LONG_T = {"centralized": 100.0, "consensus-admm": 100.0, "dual-decomposition": 10.0}
+LONG_T = {"centralized": 100.0, "consensus-admm": 100.0, "dual-decomposition": 100.0}
 
 
 def gen_long_closed_loop(name, T=None, state_every=10):
@@ -411,8 +411,92 @@ def gen_long_closed_loop(name, T=None, state_every=10):
                         x_err=np.array(xe), v_err=np.array(ve), states=np.array(xs), w=np.array(ws))
 
 
+C4_SEEDS = (0, 1, 2, 3)   # forest seeds of the four C4 closed loops
+C4_T = 4.0                # seconds (400 HL steps)
+
+
+def _terrain_z(env, xy):
+    """z of the desired-acceleration law's reference height (example/rqp_example.py:38-46) at xy."""
+    nrm = np.linalg.norm(np.asarray(xy) - env.mountain_center)
+    if nrm >= env.mountain_radius:
+        return 1.5
+    return np.sqrt(env.mountain_sphere_radius ** 2 - nrm ** 2) - env.mountain_center_depth + 1.5
+
+
+def c4_start_state(env, n, rng):
+    """Config C4 near-tree start: payload 1.6-2.8 m (xy) from the axis of a tree near the forest's
+    y = 0 line (where the desired law steers), heading at it within +-0.3 rad at 0.5-1.0 m/s, at the
+    reference height, rest attitude; positions closer than 1.5 m to any tree axis are redrawn."""
+    inner = np.nonzero((env.tree_pos[:, 0] > 8.0) & (env.tree_pos[:, 0] < 50.0) & (np.abs(env.tree_pos[:, 1]) < 4.0))[0]
+    while True:
+        k = rng.choice(inner)
+        th = rng.uniform(-0.3, 0.3)
+        head = np.array([np.cos(th), np.sin(th)])
+        xy = env.tree_pos[k, :2] - rng.uniform(1.6, 2.8) * head
+        if np.min(np.linalg.norm(env.tree_pos[:, :2] - xy, axis=1)) >= 1.5:
+            break
+    sp = rng.uniform(0.5, 1.0)
+    return RQPState(np.stack([np.eye(3)] * n, axis=2), np.zeros((3, n)), np.array([xy[0], xy[1], _terrain_z(env, xy)]),
+                    np.array([sp * head[0], sp * head[1], 0.0]), np.eye(3), np.zeros(3))
+
+
+def gen_c4_loop(T=C4_T, out_dir=None):
+    """The headline configuration's closed loop over many HL steps: n = 6
+    C-ADMM (hexagon team, oracle/scenarios.py geometry, reference RQPParameters / RQPCollision) in the
+    seeded forests C4_SEEDS, rqp_example's loop (example/rqp_example.py:120-131: forest desired
+    acceleration, RQPCADMMController.control control/rqp_cadmm.py:631-675, LL "pd", integrate; HL
+    every 10 steps) from near-tree starts for T seconds.  Recorded per HL step: f_des, iter,
+    min_env_dist, err_seq; the state at every HL instant (before its control call)."""
+    from example.rqp_example import _desired_acceleration_forest  # noqa: E402 (matplotlib import)
+    from oracle import scenarios as osc
+
+    n, dt, hl = 6, 1e-3, 10
+    m, J, ml, Jl, r = osc.geometry(n)
+    p = RQPParameters(m, J, ml, Jl, r)
+    R0 = np.linalg.norm(r, axis=0).max()
+    from system.rigid_quadrotor_payload import RQPCollision
+
+    # the build's n = 6 collision data (scenarios.collision: radius from the max mesh-vertex norm R0 +
+    # 0.1, system/rigid_quadrotor_payload.py:302-306); the reference builds a hull of the mesh, so the
+    # flat ring gets an inner, lower copy (norms < R0 + 0.1: the radius is unchanged)
+    mesh = r.T * (R0 + 0.1) / R0
+    col = RQPCollision(np.vstack([r.T, r.T - [0, 0, 0.1]]), np.vstack([mesh, 0.5 * mesh - [0, 0, 0.1]]))
+    rng = np.random.default_rng(606)
+    out = {"seeds": np.array(C4_SEEDS), "T": T, "dt": dt, "hl_rel_freq": hl}
+    steps = int(round(T / dt))
+    for k, seed in enumerate(C4_SEEDS):
+        np.random.seed(seed)
+        env = Forest()
+        s0 = c4_start_state(env, n, rng)
+        dyn = RQPDynamics(p, s0, dt)
+        ctl = RQPCADMMController(p, col, s0, dt, env)
+        ll = RQPLowLevelController("pd", p, ctl.get_force_cone_angle_bound())
+        fdes, its, mds, xs, errs = [], [], [], [], []
+        for i in range(steps):
+            if i % hl == 0:
+                s = dyn.state
+                xs.append(np.concatenate([s.R.reshape(-1), s.w.reshape(-1), s.xl, s.vl, s.Rl.reshape(-1), s.wl]))
+                acc, _, _ = _desired_acceleration_forest(dyn.state, i * dt, env)
+                f_des, st = ctl.control(dyn.state, acc)
+                fdes.append(f_des.copy()), its.append(st.iter), mds.append(st.min_env_dist)
+                errs.append(np.pad(np.array(st.err_seq, float), (0, 101 - len(st.err_seq)), constant_values=np.nan))
+            dyn.integrate(ll.control(dyn.state, f_des))
+            refstubs.TRACE.clear()
+        out[f"s{k}_f_des"], out[f"s{k}_iters"] = np.array(fdes), np.array(its, dtype=np.int16)
+        out[f"s{k}_min_dist"], out[f"s{k}_states"] = np.array(mds), np.array(xs)
+        out[f"s{k}_err"] = np.array(errs)[:, :8]  # the first 8 residuals of each step (C4 steps take 1-5)
+        print(f"c4 loop {k}: min dist {min(mds):.3f}, iters {np.bincount(its)}", flush=True)
+    np.savez_compressed(os.path.join(out_dir or OUT, "ref_c4_loop.npz"), **out)
+
+
 if __name__ == "__main__":
     import time
+
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":
+        t = time.time()
+        gen_c4_loop()
+        print(f"gen_c4_loop: {time.time() - t:.1f}s", flush=True)
+        sys.exit(0)
 
     if len(sys.argv) > 1 and sys.argv[1] == "rp":
         gen_rp()

@@ -34,10 +34,11 @@ from oracle import model as omodel
 # ============================================================================ cvxpy tracing stub
 _REGISTRY = []  # all Variables in creation order
 TRACE = []      # recorded problem data of every Problem.solve
+_NX = [0]       # total size of the registered Variables (kept in step with _REGISTRY)
 
 
 def _nx():
-    return sum(v.size for v in _REGISTRY)
+    return _NX[0]
 
 
 class Expr:
@@ -54,7 +55,10 @@ class Expr:
 
     @property
     def size(self):
-        return int(np.prod(self.shape)) if self.shape else 1
+        n = 1
+        for d in self.shape:
+            n *= int(d)
+        return n
 
     @property
     def ndim(self):
@@ -231,6 +235,7 @@ class Variable(Expr):
 
         super().__init__(shape, ev)
         _REGISTRY.append(self)
+        _NX[0] += self.size
 
     @property
     def value(self):

@@ -45,6 +45,24 @@ def qp_cadmm(prm, n, st, acc, lhs, rhs, i, lam, fbar, rho=1.0):
     return f, status, it.value
 
 
+def qp_cadmm_ex(prm, n, st, acc, lhs, rhs, i, lam, fbar, rho=1.0, tuned=0):
+    """hs_qp_cadmm with the IPM start flag of k_cadmm; returns (f, status, iters, inband)"""
+    f = np.zeros(3 * n)
+    it, ib = ctypes.c_int(), ctypes.c_int()
+    lhs = np.ascontiguousarray(lhs, dtype=np.float64).reshape(-1, 3)
+    status = lib().hs_qp_cadmm_ex(p(prm), n, p(st), p(acc), p(lhs), p(rhs), lhs.shape[0], i, p(lam), p(fbar),
+                                  ctypes.c_double(rho), int(tuned), f.ctypes.data_as(D), ctypes.byref(it),
+                                  ctypes.byref(ib))
+    return f, status, it.value, ib.value
+
+
+def last_diag():
+    """(merit, inband, exit reason) of the last hostsim QP solve"""
+    m, ib, why = ctypes.c_double(), ctypes.c_int(), ctypes.c_int()
+    lib().hs_last_diag(ctypes.byref(m), ctypes.byref(ib), ctypes.byref(why))
+    return m.value, ib.value, why.value
+
+
 def qp_dd(prm, n, st, acc, lhs, rhs, i, c9):
     x = np.zeros(9)
     it = ctypes.c_int()

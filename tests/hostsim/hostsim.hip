@@ -27,8 +27,17 @@ void env_slots(const double* env_lhs, const double* env_rhs, int nenv, double lh
     }
   }
 }
+// diagnostics of the last solve (hs_last_diag)
+double g_merit = 0.0;
+int g_inband = 0, g_why = 0;
+void diag(const IPMOut& o) {
+  g_merit = o.merit;
+  g_inband = o.inband;
+  g_why = o.why;
+}
+
 template <int NB>
-int cent_nb(const double* prm, const double* st, const double* acc, const double* env_lhs, const double* env_rhs,
+int cent_nb_(const double* prm, const double* st, const double* acc, const double* env_lhs, const double* env_rhs,
             int nenv, double* f_out, int* iters) {
   QPShared S;
   build_shared(S, prm, NB, st, acc, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
@@ -43,6 +52,7 @@ int cent_nb(const double* prm, const double* st, const double* acc, const double
   double y[NB][3], w[6], best[best_size(NB)];
   IPMOut o = ipm_solve_rows<MODE_CENT, NB>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
                                            RtPtr{&Rt[0][0]}, P, prm + DAT_P_FEQ(NB), y, w, best, 50, HS_TOL);
+  diag(o);
   for (int k = 0; k < NB; ++k)
     for (int c = 0; c < 3; ++c) f_out[3 * k + c] = y[k][c];
   *iters = o.iters;
@@ -53,9 +63,25 @@ int cent_nb(const double* prm, const double* st, const double* acc, const double
 
 extern "C" {
 
+void hs_last_diag(double* merit, int* inband, int* why) {
+  *merit = g_merit;
+  *inband = g_inband;
+  *why = g_why;
+}
+
+int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
+                   const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
+                   int tuned, double* f_out, int* iters, int* inband);
 int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                 const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
                 double* f_out, int* iters) {
+  int ib = 0;
+  return hs_qp_cadmm_ex(prm, n, st, acc, env_lhs, env_rhs, nenv, i, lam, fbar, rho, 0, f_out, iters, &ib);
+}
+// as hs_qp_cadmm with k_cadmm's IPM start policy flag (P.tuned) and the in-band exit flag out
+int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
+                   const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
+                   int tuned, double* f_out, int* iters, int* inband) {
   if (nenv > DAT_NENV) return -1;
   double Rt_all[16 * 9];
   const double* Rl = st + DAT_S_RL(n);
@@ -70,10 +96,13 @@ int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, c
   EnvRows E;
   set_env_rows(P, E, S, mask, lhs, rhs);
   lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
+  P.tuned = tuned;
   double y[1][3], w[6], best[best_size(1)];
   IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
                                            RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50,
                                            HS_TOL);
+  *inband = o.inband ? 10 * o.why + 1 : 0;
+  diag(o);
   for (int j = 0; j < n; ++j) {
     if (j == i) {
       for (int c = 0; c < 3; ++c) f_out[3 * j + c] = y[0][c];
@@ -103,6 +132,7 @@ int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, cons
   double y[1][3], w[6], best[best_size(1)];
   IPMOut o = ipm_solve_rows<MODE_DD, 1>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
                                         RtPtr{Rt}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50, HS_TOL);
+  diag(o);
   for (int c = 0; c < 3; ++c) x_out[c] = y[0][c];
   for (int c = 0; c < 6; ++c) x_out[3 + c] = w[c];
   *iters = o.iters;
@@ -112,8 +142,8 @@ int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, cons
 int hs_qp_cent(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                const double* env_rhs, int nenv, double* f_out, int* iters) {
   if (nenv > DAT_NENV) return -1;
-  if (n == 3) return cent_nb<3>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
-  if (n == 6) return cent_nb<6>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
+  if (n == 3) return cent_nb_<3>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
+  if (n == 6) return cent_nb_<6>(prm, st, acc, env_lhs, env_rhs, nenv, f_out, iters);
   return -1;
 }
 

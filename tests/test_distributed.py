@@ -78,3 +78,31 @@ def test_bench_spawns_ranks_selftest():
     assert out["stats"]["agent_qp_solves"] == 2 * 2 * 16 * 6  # ranks x steps x scenarios x agents
     assert out["stats"]["mean_admm_iters"] == 1.5             # gathered from both ranks (1 and 2)
     assert out["data"].startswith("selftest")
+
+
+def test_strong_shard_partitions_the_total():
+    for total, world in ((65536, 8), (65536, 1), (32, 2), (35, 4)):
+        parts = [bench.strong_shard(r, world, total) for r in range(world)]
+        ids = np.concatenate([np.arange(lo, lo + c) for lo, c in parts])
+        assert np.array_equal(ids, np.arange(total))
+        assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+    assert bench.strong_shard(3, 8, 65536) == (3 * 8192, 8192)  # BASELINE configs[3]: 8,192 per GPU
+
+
+def test_bench_strong_scaling_selftest():
+    """`bench.py --gpus 2 --selftest --total-batch 32`: strong scaling, 16 scenarios per rank, 32 in total."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--selftest", "--steps", "2",
+                        "--warmup", "1", "--total-batch", "32"], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["scaling"] == "strong"
+    assert out["config"]["scenarios_per_gpu"] == 16 and out["config"]["total_scenarios"] == 32
+    assert out["stats"]["agent_qp_solves"] == 2 * 2 * 16 * 6  # ranks x steps x scenarios per rank x agents

@@ -130,6 +130,8 @@ def test_c4_all_scenarios_sane(c4_run):
     assert env_qps > 0.5 * c4_run["work"]["qp_solves"], c4_run["classes"]
     # slot refill: more scenarios than the 2 x 10 resident slots, all completed
     assert c4_run["work"]["qp_solves"] >= 2 * c4_run["B"] * N
+    # every agent QP converged to the IPM tolerance (none accepted through the in-band best iterate)
+    assert c4_run["work"]["inband_beyond_clarabel_tol"] == 0
 
 
 def test_c4_sample_matches_oracle(c4_run):

@@ -120,6 +120,10 @@ def test_gpu_primal_solver_dropins_and_fallbacks():
         ps = RQPCADMMPrimalSolver(p, col, int(d[f"cadmm{k}_i"]), s, 1e-3)
         f, t, coll, md = ps.solve(s, acc, d[f"cadmm{k}_lam"], 1.0, d[f"cadmm{k}_fm"])
         assert _rel(f, d[f"cadmm{k}_x"][9:].reshape(3, 3, order="F")) < REL
+        assert 0.0 < t < 1.0  # the QP kernel's device time [s] (Clarabel's solve_time, control/rqp_cadmm.py:500)
+        # rho = 0 (the reference's default, used only by its constructor's warm-up solve) is rejected
+        with pytest.raises(ValueError):
+            ps.solve(s, acc, d[f"cadmm{k}_lam"])
         # payload upside down: the tilt CBF row 0 . dwl >= cos 15 deg - Rl[2,2] > 0 is infeasible -> hold
         bad = system.RQPState.unpack(_pack(state_from(d, f"cadmm{k}_s_")), 3)
         bad.Rl = np.diag([1.0, -1.0, -1.0])
@@ -139,6 +143,7 @@ def test_gpu_primal_solver_dropins_and_fallbacks():
         cc = d[f"dd{k}_c"]
         fi, Fi, Mi, t, coll, md = ps.solve(s, acc, cc[:3], cc[3:6], cc[6:])
         assert _rel(np.concatenate([fi, Fi, Mi]), d[f"dd{k}_x"][9:]) < REL
+        assert 0.0 < t < 1.0
         nan = system.RQPState.unpack(_pack(state_from(d, f"dd{k}_s_")), 3)
         nan.vl = np.full(3, np.nan)
         fi, Fi, Mi, *_ = ps.solve(nan, acc, cc[:3], cc[3:6], cc[6:])

@@ -94,6 +94,7 @@ def test_gpu_cadmm_step_matches_oracle(n):
         assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL
         np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=1e-4, atol=1e-6)
         assert np.all(r1.qp_status[b] == 0)
+    assert eng.work()["inband_beyond_clarabel_tol"] == 0
 
 
 def test_gpu_cadmm_convergence_recipe_golden():
@@ -160,6 +161,7 @@ def test_gpu_dd_step_matches_oracle(n):
         np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
         assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
     assert skipped <= 1
+    assert eng.work()["inband_beyond_clarabel_tol"] == 0
 
 
 def _random_mass_params(n, B, rng):
@@ -346,6 +348,7 @@ def test_gpu_dd_persistent_drain():
         eng = _eng("dd", n, B, record_err=True)
         eng.set_persistent_blocks(blocks)
         runs.append((eng.control(states, a1), eng.control(states, a2)))
+        assert eng.work()["inband_beyond_clarabel_tol"] == 0
     for r_cap, r_full in zip(*runs):
         np.testing.assert_array_equal(r_cap.f_des, r_full.f_des)
         np.testing.assert_array_equal(r_cap.iters, r_full.iters)
