@@ -185,9 +185,11 @@ __host__ __device__ inline bool cadmm_rows_lds(int n, int G, int cls) {
   if (cls >= NCLS - 1 || cls < ROWLDS_MIN_CLS) return false;
   return cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
 }
-__host__ __device__ inline size_t cadmm_lds_bytes(int n, int G) {
+// dynamic LDS of a k_cadmm workgroup: the largest carve of the env classes that can occur (without a
+// forest every scenario is class 0, so the launch needs only that carve and more workgroups fit a CU)
+__host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NCLS - 1) {
   size_t m = 0;
-  for (int c = 0; c < NCLS; ++c) {
+  for (int c = 0; c <= max_cls; ++c) {
     const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_rows_lds(n, G, c));
     m = b > m ? b : m;
   }
@@ -246,9 +248,12 @@ __device__ inline int env_class_of(unsigned emask, const double lhs[DAT_NENV][3]
 // order as env_rows (the rows are bitwise identical; test_gpu_env_rows / test_gpu_c4).
 // Must be called by every lane of the block (barriers inside).
 constexpr int ENV_CE = 8;  // published entry: in range, c.x, c.y, dd, l3[3], r1
+// LDS stride of a published entry: 9 doubles (18 dwords), so the 32 lanes of a ds_*_b64 half-wave
+// start on 32 distinct even banks (a stride of 8 doubles put 64 lanes on 4 bank pairs: 16-way conflicts)
+constexpr int ENV_CS = ENV_CE + 1;
 __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, const double* trees, int ntree, int i,
                                 int ls, bool valid, double alpha_env, unsigned* mask, double lhs[DAT_NENV][3],
-                                double rhs[DAT_NENV], double* ent /* LDS: 64 x ENV_CE */) {
+                                double rhs[DAT_NENV], double* ent /* LDS: 64 x ENV_CS */) {
   EnvOut out;
   out.collision = 0;
   out.min_env_dist = valid ? prm[DAT_P_VISR] : 0.0;
@@ -303,8 +308,8 @@ __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, cons
   for (int j = 0; j < DAT_NENV; ++j) bd[j] = 1e300;
   int cnt = 0;
   double dmin = 1e300;
-  double* mine = ent + (size_t)threadIdx.x * ENV_CE;
-  const double* grp = ent + (size_t)(ls * n) * ENV_CE;
+  double* mine = ent + (size_t)threadIdx.x * ENV_CS;
+  const double* grp = ent + (size_t)(ls * n) * ENV_CS;
   for (int base = t0;; base += n) {
     // this lane's tree of the chunk
     const int t = base + i;
@@ -340,7 +345,7 @@ __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, cons
     __syncthreads();
     if (!dead) {
       for (int j = 0; j < n; ++j) {  // the chunk in tree order
-        const double* q = grp + (size_t)j * ENV_CE;
+        const double* q = grp + (size_t)j * ENV_CS;
         if (q[0] == 0.0) continue;
         const double tx = q[1] - cam[0], ty = q[2] - cam[1];
         const double nn = sqrt(tx * tx + ty * ty);
@@ -387,7 +392,7 @@ __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, cons
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_env_class(KArgs a) {
   __shared__ int nd[64], cl[64];
   __shared__ double md[64];
-  __shared__ double ent[64 * ENV_CE];
+  __shared__ double ent[64 * ENV_CS];
   const int n = a.n, G = 64 / n, NT = G * n;
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
@@ -1702,8 +1707,8 @@ int launch_hl(dat_handle* h) {
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
     const int Gc = a.G, cblocks = (B + Gc - 1) / Gc;
-    hipLaunchKernelGGL(k_cadmm, dim3(std::min(cblocks, h->persistent_blocks)), dim3(64), cadmm_lds_bytes(n, Gc),
-                       h->stream, a);
+    hipLaunchKernelGGL(k_cadmm, dim3(std::min(cblocks, h->persistent_blocks)), dim3(64),
+                       cadmm_lds_bytes(n, Gc, h->nforest > 0 ? NCLS - 1 : 0), h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
     hipLaunchKernelGGL(k_dd_key, dim3((B + 63) / 64), dim3(64), 0, h->stream, a);

@@ -485,20 +485,23 @@ DAT_HD double soc_step(const double* x, const double* d) {
 // (slot l of lane j: s at [l 64 + j], z at [(NR + l) 64 + j], zw at [(2 NR + l) 64 + j]; a
 // wavefront reading one slot touches 64 consecutive doubles, bank-conflict free), read and written
 // through an index the compiler cannot see through, so the rows cost no registers between uses.
+// Besides the rows, a store may hold NX auxiliary per-lane doubles (aux slots: the per-iteration
+// quantities ipm_solve's AUXM mask moves out of the register file, see ipm_aux_doubles).
 struct RowRegs {
-  template <int NR>
+  template <int NR, int NX = 0>
   struct Store {
-    double s_[NR], z_[NR], w_[NR];
+    double s_[NR], z_[NR], w_[NR], x_[NX > 0 ? NX : 1];
     DAT_HD explicit Store(const RowRegs&) {}
     DAT_HD double& s(int l) { return s_[l]; }
     DAT_HD double& z(int l) { return z_[l]; }
     DAT_HD double& w(int l) { return w_[l]; }
+    DAT_HD double& x(int k) { return x_[k]; }
   };
 };
 struct RowLds {
   double* base;
   int lane;
-  template <int NR>
+  template <int NR, int NX = 0>
   struct Store {
     DAT_LDS double* p;  // the lane's column
     __device__ explicit Store(const RowLds& r) : p((DAT_LDS double*)(r.base + r.lane)) {}
@@ -506,9 +509,34 @@ struct RowLds {
     __device__ volatile DAT_LDS double& s(int l) { return at(l); }
     __device__ volatile DAT_LDS double& z(int l) { return at(NR + l); }
     __device__ volatile DAT_LDS double& w(int l) { return at(2 * NR + l); }
+    __device__ volatile DAT_LDS double& x(int k) { return at(3 * NR + k); }
   };
 };
-__host__ __device__ constexpr int row_lds_doubles(int NR) { return 3 * NR * 64; }
+// Host model of RowLds (the same strided column in ordinary memory): exercises the aux / row store
+// code paths of ipm_solve in the host build (tests/hostsim).
+struct RowMem {
+  double* base;
+  int lane;
+  template <int NR, int NX = 0>
+  struct Store {
+    double* p;
+    DAT_HD explicit Store(const RowMem& r) : p(r.base + r.lane) {}
+    DAT_HD double& at(int k) { return p[k * 64]; }
+    DAT_HD double& s(int l) { return at(l); }
+    DAT_HD double& z(int l) { return at(NR + l); }
+    DAT_HD double& w(int l) { return at(2 * NR + l); }
+    DAT_HD double& x(int k) { return at(3 * NR + k); }
+  };
+};
+// aux slots of ipm_solve (AUXM bits): SCAL the stopping-rule scales and best merits (4), RES the
+// iteration's residuals r_y and R_f (3 NB + 6), LAM the scaled point lambda = W z (9 NB), DINV the
+// cone blocks' D^-1 and 1 / d0 (7 NB)
+constexpr unsigned AUX_SCAL = 1, AUX_RES = 2, AUX_LAM = 4, AUX_DINV = 8;
+__host__ __device__ constexpr int ipm_aux_doubles(int NB, unsigned AUXM) {
+  return ((AUXM & AUX_SCAL) ? 4 : 0) + ((AUXM & AUX_RES) ? 3 * NB + 6 : 0) + ((AUXM & AUX_LAM) ? 9 * NB : 0) +
+         ((AUXM & AUX_DINV) ? 7 * NB : 0);
+}
+__host__ __device__ constexpr int row_lds_doubles(int NR, int NX = 0) { return (3 * NR + NX) * 64; }
 
 struct IPMOut {
   int status;
@@ -534,10 +562,18 @@ struct IPMOut {
 // row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
-template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs>
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{}) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
+  // aux slot offsets (only the AUXM groups are allocated)
+  constexpr int O_SC = 0;
+  constexpr int O_RK = O_SC + ((AUXM & AUX_SCAL) ? 4 : 0);
+  constexpr int O_RF = O_RK + 3 * NB;
+  constexpr int O_LAM = O_RK + ((AUXM & AUX_RES) ? 3 * NB + 6 : 0);
+  constexpr int O_DI = O_LAM + ((AUXM & AUX_LAM) ? 9 * NB : 0);
+  constexpr int O_ID0 = O_DI + 6 * NB;
+  constexpr int NX = ipm_aux_doubles(NB, AUXM);
   IPMOut out;
   out.status = ST_FAILED;
   out.iters = 0;
@@ -642,9 +678,49 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   const double mfz = P.min_fz, mxf = P.max_f;
   // primal residual of cone block k at the current iterate: G y + s - h
   double sk[NB][9], zk[NB][9];
-  typename RW::template Store<NR> rst(rw);  // row slacks / duals / Newton row terms (registers or LDS)
+  typename RW::template Store<NR, NX> rst(rw);  // row slacks / duals / Newton row terms (registers or LDS)
   auto SL = [&](int l) -> decltype(auto) { return rst.s(l); };
   auto ZL = [&](int l) -> decltype(auto) { return rst.z(l); };
+  // per-iteration quantities: registers, or the store's aux slots (AUXM)
+  double nh_r = 0.0, nq_r = 0.0, bm_r = 0.0, bk_r = 0.0;
+  double rk_r[(AUXM & AUX_RES) ? 1 : 3 * NB], rf_r[(AUXM & AUX_RES) ? 1 : 6];
+  double lam_r[(AUXM & AUX_LAM) ? 1 : 9 * NB];
+  double di_r[(AUXM & AUX_DINV) ? 1 : 6 * NB], id0_r[(AUXM & AUX_DINV) ? 1 : NB];
+  auto NH = [&]() -> decltype(auto) {
+    if constexpr ((AUXM & AUX_SCAL) != 0) return rst.x(O_SC + 0); else return (nh_r);
+  };
+  auto NQ = [&]() -> decltype(auto) {
+    if constexpr ((AUXM & AUX_SCAL) != 0) return rst.x(O_SC + 1); else return (nq_r);
+  };
+  auto BM = [&]() -> decltype(auto) {  // best merit seen (divergence stop)
+    if constexpr ((AUXM & AUX_SCAL) != 0) return rst.x(O_SC + 2); else return (bm_r);
+  };
+  auto BK = [&]() -> decltype(auto) {  // merit of the recorded in-band iterate
+    if constexpr ((AUXM & AUX_SCAL) != 0) return rst.x(O_SC + 3); else return (bk_r);
+  };
+  auto RK = [&](int k, int c) -> decltype(auto) {
+    if constexpr ((AUXM & AUX_RES) != 0) return rst.x(O_RK + 3 * k + c); else return (rk_r[3 * k + c]);
+  };
+  auto RF = [&](int r) -> decltype(auto) {
+    if constexpr ((AUXM & AUX_RES) != 0) return rst.x(O_RF + r); else return (rf_r[r]);
+  };
+  auto LAM = [&](int k, int j) -> decltype(auto) {
+    if constexpr ((AUXM & AUX_LAM) != 0) return rst.x(O_LAM + 9 * k + j); else return (lam_r[9 * k + j]);
+  };
+  auto DI = [&](int k, int j) -> decltype(auto) {
+    if constexpr ((AUXM & AUX_DINV) != 0) return rst.x(O_DI + 6 * k + j); else return (di_r[6 * k + j]);
+  };
+  auto ID0 = [&](int k) -> decltype(auto) {
+    if constexpr ((AUXM & AUX_DINV) != 0) return rst.x(O_ID0 + k); else return (id0_r[k]);
+  };
+  auto lam4 = [&](int k, int j0, double* o) {  // lambda_k[j0 .. j0 + 3]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = LAM(k, j0 + j);
+  };
+  auto dinv = [&](int k, double* o) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) o[j] = DI(k, j);
+  };
   auto rzk_of = [&](int k, double* o) {
     Gy(y[k], o);
 #pragma unroll
@@ -715,25 +791,29 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   }
 
   // scales for the relative stopping rule
-  double nh = 1.0 + fmax(mfz, mxf), nq = 1.0;
+  {
+    double nh = 1.0 + fmax(mfz, mxf), nq = 1.0;
 #pragma unroll
-  for (int l = 0; l < NR; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
+    for (int l = 0; l < NR; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
 #pragma unroll
-  for (int k = 0; k < NB; ++k)
+    for (int k = 0; k < NB; ++k)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) nq = fmax(nq, 1.0 + fabs(P.q[k][c]));
+      for (int c = 0; c < 3; ++c) nq = fmax(nq, 1.0 + fabs(P.q[k][c]));
 #pragma unroll
-  for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
+    for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
+    NH() = nh;
+    NQ() = nq;
+  }
 
   // best in-band iterate (merit of the recorded one) and the best merit seen (divergence stop)
-  double best_merit = 1e300, best_key = 1e300;
+  BM() = 1e300;
+  BK() = 1e300;
   out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
   const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
 
   for (int it = 0;; ++it) {
     // ------------- residuals
     double dv[3], dw[3];
-    double rk[NB][3], Rf[6];
     double dres = 0.0, pres = 0.0, gap = 0.0;
     double chk = 0.0;  // plain sum of every residual entry: NaN / Inf propagate (fmax drops NaN)
     {
@@ -751,27 +831,32 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         GTz(zk[k], gz);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          rk[k][c] = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
-          dres = fmax(dres, fabs(rk[k][c]));
-          chk += rk[k][c];
+          const double r = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
+          RK(k, c) = r;
+          dres = fmax(dres, fabs(r));
+          chk += r;
         }
       }
-      if (MODE == MODE_CADMM) {
-        double kp[6];
-        Kmul(pi, kp);
+      {
+        double Rf[6];
+        if (MODE == MODE_CADMM) {
+          double kp[6];
+          Kmul(pi, kp);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) Rf[r] = P.rho * (w[r] - P.atil[r]) + kp[r];
-      } else if (MODE == MODE_DD) {
+          for (int r = 0; r < 6; ++r) Rf[r] = P.rho * (w[r] - P.atil[r]) + kp[r];
+        } else if (MODE == MODE_DD) {
 #pragma unroll
-        for (int r = 0; r < 6; ++r) Rf[r] = pi[r] + P.cw[r];
-      } else {
+          for (int r = 0; r < 6; ++r) Rf[r] = pi[r] + P.cw[r];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 6; ++r) Rf[r] = 0.0;
-      }
+          for (int r = 0; r < 6; ++r) Rf[r] = 0.0;
+        }
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        dres = fmax(dres, fabs(Rf[r]));
-        chk += Rf[r];
+        for (int r = 0; r < 6; ++r) {
+          RF(r) = Rf[r];
+          dres = fmax(dres, fabs(Rf[r]));
+          chk += Rf[r];
+        }
       }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -799,6 +884,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         out.why = 1;
         break;
       }
+      const double nh = NH(), nq = NQ();
       double merit = fmax(fmax(pres / nh, dres / nq), gap);
 #ifdef DAT_IPM_TRACE
       printf("ipm it %2d pres %.3e dres %.3e gap %.3e merit %.3e\n", it, pres / nh, dres / nq, gap, merit);
@@ -815,8 +901,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       // out-of-band iterates are never recorded (the record is written in the last one or two
       // iterations of a stalling solve, not at every iteration).
       const bool band = fmax(pres / nh, dres / nq) < 1e-7 && gap < 1e-6;
-      if (band && merit < best_key) {
-        best_key = merit;
+      if (band && merit < BK()) {
+        BK() = merit;
 #pragma unroll
         for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -828,8 +914,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           best[3 * NB + 12 + r] = u[r];
         }
       }
-      best_merit = fmin(best_merit, merit);
-      if ((it >= 4 && merit > DAT_IPM_DIVERGE * best_merit) || it >= max_iter) {
+      BM() = fmin(BM(), merit);
+      if ((it >= 4 && merit > DAT_IPM_DIVERGE * BM()) || it >= max_iter) {
         out.why = 2;
         break;
       }
@@ -838,22 +924,24 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 
     // ------------- NT scaling of the cone blocks
     SocScale S1[NB], S2[NB];
-    double id0[NB], lamk[NB][9];
     bool okc = true;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      id0[k] = sqrt(zk[k][0] * frcp(sk[k][0]));  // 1 / d0, d0 = sqrt(s0 / z0)
-      lamk[k][0] = sqrt(sk[k][0] * zk[k][0]);
+      ID0(k) = sqrt(zk[k][0] * frcp(sk[k][0]));  // 1 / d0, d0 = sqrt(s0 / z0)
+      LAM(k, 0) = sqrt(sk[k][0] * zk[k][0]);
       okc = okc && soc_scaling(sk[k] + 1, zk[k] + 1, S1[k]) && soc_scaling(sk[k] + 5, zk[k] + 5, S2[k]);
-      soc_apply(S1[k], zk[k] + 1, lamk[k] + 1, false);
-      soc_apply(S2[k], zk[k] + 5, lamk[k] + 5, false);
+      double l1[4], l2[4];
+      soc_apply(S1[k], zk[k] + 1, l1, false);
+      soc_apply(S2[k], zk[k] + 5, l2, false);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { LAM(k, 1 + j) = l1[j]; LAM(k, 5 + j) = l2[j]; }
     }
     if (!okc) {
       out.why = 3;
       break;
     }
     auto winv = [&](int k, const double* v, double* o) {  // W_k^-1 v
-      o[0] = v[0] * id0[k];
+      o[0] = v[0] * ID0(k);
       soc_apply(S1[k], v + 1, o + 1, true);
       soc_apply(S2[k], v + 5, o + 5, true);
     };
@@ -869,7 +957,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       GTz(g, o);
     };
     // D_k = kappa I + Gs'Gs (packed) and its inverse
-    double Dinv[NB][6];
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       double gc[3][9];
@@ -888,7 +975,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           for (int j = 0; j < 9; ++j) s += gc[r][j] * gc[c][j];
           D[sp3(r, c)] = s;
         }
-      okc = okc && inv3_spd(D, Dinv[k]);
+      double Di[6];
+      okc = okc && inv3_spd(D, Di);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) DI(k, j) = Di[j];
     }
     if (!okc) {
       out.why = 4;
@@ -957,13 +1047,17 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
           // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
-          double Dm[6] = {Dinv[0][0] - irho, Dinv[0][1], Dinv[0][2], Dinv[0][3] - irho, Dinv[0][4], Dinv[0][5] - irho};
+          double Dm[6] = {DI(0, 0) - irho, DI(0, 1), DI(0, 2), DI(0, 3) - irho, DI(0, 4), DI(0, 5) - irho};
           add_UDUt(T, rt.get(0), Dm, 1.0);
         } else {
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = 0.0;
 #pragma unroll
-          for (int k = 0; k < NB; ++k) add_UDUt(T, rt.get(k), Dinv[k], 1.0);
+          for (int k = 0; k < NB; ++k) {
+            double Di[6];
+            dinv(k, Di);
+            add_UDUt(T, rt.get(k), Di, 1.0);
+          }
         }
         double Nn[21], Ln[21];
         ltl_plus_identity(Lm, T, Nn);
@@ -993,7 +1087,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           Ut_apply(rt.get(k), Rfr, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) v[c] = bk[k][c] + t[c];
-          spmv3(Dinv[k], v, dyn[k]);
+          double Di[6];
+          dinv(k, Di);
+          spmv3(Di, v, dyn[k]);
         }
 #pragma unroll
         for (int r = 0; r < 6; ++r) dwn[r] = dun[r];
@@ -1012,7 +1108,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           if (has_bu) Ut_apply(rt.get(k), bu, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) bk2[k][c] = bk[k][c] + t[c];
-          spmv3(Dinv[k], bk2[k], v);
+          double Di[6];
+          dinv(k, Di);
+          spmv3(Di, bk2[k], v);
           U_apply(rt.get(k), v, ut);
 #pragma unroll
           for (int r = 0; r < 6; ++r) yv[r] += ut[r];
@@ -1034,7 +1132,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           Ut_apply(rt.get(k), tau, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) v[c] = bk2[k][c] - t[c];
-          spmv3(Dinv[k], v, dyn[k]);
+          double Di[6];
+          dinv(k, Di);
+          spmv3(Di, v, dyn[k]);
         }
         if (MODE == MODE_CADMM) {
           double kt[6];
@@ -1085,14 +1185,19 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       double bk[NB][3], bu[6];
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
-        lrs_k[k][0] = rsk[k][0] * frcp(lamk[k][0]);
-        soc_jdiv(lamk[k] + 1, rsk[k] + 1, lrs_k[k] + 1);
-        soc_jdiv(lamk[k] + 5, rsk[k] + 5, lrs_k[k] + 5);
+        lrs_k[k][0] = rsk[k][0] * frcp(LAM(k, 0));
+        {
+          double l4[4];
+          lam4(k, 1, l4);
+          soc_jdiv(l4, rsk[k] + 1, lrs_k[k] + 1);
+          lam4(k, 5, l4);
+          soc_jdiv(l4, rsk[k] + 5, lrs_k[k] + 5);
+        }
         double tks[9], g3[3];
         tks_of(k, tks);
         gs_tmul(k, tks, g3);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) bk[k][c] = -rk[k][c] - g3[c];
+        for (int c = 0; c < 3; ++c) bk[k][c] = -RK(k, c) - g3[c];
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
@@ -1106,7 +1211,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         ZW(l) = (ZL(l) * rzl - (SL(l) * ZL(l) + cadd)) * is;
       }
       rows_adj(ZW, bu);
-      core(bk, Rf, bu, true, false, dy, dwv, du);
+      {
+        double rfv[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) rfv[r] = RF(r);
+        core(bk, rfv, bu, true, false, dy, dwv, du);
+      }
       // the affine (predictor) direction only sets the step length, sigma and the corrector's
       // second-order term: it is used unrefined; the corrector -- the step actually taken -- is refined
       const int nref = corr ? NREF : 0;
@@ -1145,16 +1255,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           Ut_apply(rt.get(k), dpi, ut);
           gs_tmul(k, dzs_k[k], g3);
 #pragma unroll
-          for (int c = 0; c < 3; ++c) ek[k][c] = -(kap * dy[k][c] + ut[c] + g3[c] + rk[k][c]);
+          for (int c = 0; c < 3; ++c) ek[k][c] = -(kap * dy[k][c] + ut[c] + g3[c] + RK(k, c));
         }
         if (MODE == MODE_CADMM) {
           double kp[6];
           Kmul(dpi, kp);
 #pragma unroll
-          for (int r = 0; r < 6; ++r) ef[r] = P.rho * dwv[r] + kp[r] + Rf[r];
+          for (int r = 0; r < 6; ++r) ef[r] = P.rho * dwv[r] + kp[r] + RF(r);
         } else if (MODE == MODE_DD) {
 #pragma unroll
-          for (int r = 0; r < 6; ++r) ef[r] = dpi[r] + Rf[r];
+          for (int r = 0; r < 6; ++r) ef[r] = dpi[r] + RF(r);
         } else {
 #pragma unroll
           for (int r = 0; r < 6; ++r) ef[r] = 0.0;
@@ -1165,9 +1275,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int k = 0; k < NB; ++k)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { en = fmax(en, fabs(ek[k][c])); sc = fmax(sc, fabs(rk[k][c])); }
+            for (int c = 0; c < 3; ++c) { en = fmax(en, fabs(ek[k][c])); sc = fmax(sc, fabs(RK(k, c))); }
 #pragma unroll
-          for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(Rf[r])); }
+          for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(RF(r))); }
 #ifndef DAT_IPM_REF_THRESH
 #define DAT_IPM_REF_THRESH 1e-12
 #endif
@@ -1198,12 +1308,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         double dss[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) dss[j] = -lrs_k[k][j] - dzs_k[k][j];
-        if (dss[0] < 0) a = fmin(a, -lamk[k][0] * frcp(dss[0]));
-        if (dzs_k[k][0] < 0) a = fmin(a, -lamk[k][0] * frcp(dzs_k[k][0]));
-        a = fmin(a, soc_step(lamk[k] + 1, dss + 1));
-        a = fmin(a, soc_step(lamk[k] + 1, dzs_k[k] + 1));
-        a = fmin(a, soc_step(lamk[k] + 5, dss + 5));
-        a = fmin(a, soc_step(lamk[k] + 5, dzs_k[k] + 5));
+        const double l0 = LAM(k, 0);
+        if (dss[0] < 0) a = fmin(a, -l0 * frcp(dss[0]));
+        if (dzs_k[k][0] < 0) a = fmin(a, -l0 * frcp(dzs_k[k][0]));
+        double l4[4];
+        lam4(k, 1, l4);
+        a = fmin(a, soc_step(l4, dss + 1));
+        a = fmin(a, soc_step(l4, dzs_k[k] + 1));
+        lam4(k, 5, l4);
+        a = fmin(a, soc_step(l4, dss + 5));
+        a = fmin(a, soc_step(l4, dzs_k[k] + 5));
       }
       double ddv[3], ddw[3];
       lin(du, ddv, ddw);
@@ -1223,7 +1337,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
           double dss = -lrs_k[k][j] - dzs_k[k][j];
-          g += (lamk[k][j] + al * dss) * (lamk[k][j] + al * dzs_k[k][j]);
+          const double lj = LAM(k, j);
+          g += (lj + al * dss) * (lj + al * dzs_k[k][j]);
         }
       double ddv[3], ddw[3];
       lin(du, ddv, ddw);
@@ -1241,9 +1356,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       double rsk[NB][9];
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
-        rsk[k][0] = lamk[k][0] * lamk[k][0];
-        soc_jprod(lamk[k] + 1, lamk[k] + 1, rsk[k] + 1);
-        soc_jprod(lamk[k] + 5, lamk[k] + 5, rsk[k] + 5);
+        const double l0 = LAM(k, 0);
+        rsk[k][0] = l0 * l0;
+        double l4[4];
+        lam4(k, 1, l4);
+        soc_jprod(l4, l4, rsk[k] + 1);
+        lam4(k, 5, l4);
+        soc_jprod(l4, l4, rsk[k] + 5);
       }
       newton(rsk, false, nullptr, nullptr, 0.0);
     }
@@ -1260,9 +1379,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         double dss[9], c1[4], c2[4];
 #pragma unroll
         for (int j = 0; j < 9; ++j) dss[j] = -lrs_k[k][j] - dzs_k[k][j];
-        rsk[k][0] = lamk[k][0] * lamk[k][0] + dss[0] * dzs_k[k][0] - sigmu;
-        soc_jprod(lamk[k] + 1, lamk[k] + 1, rsk[k] + 1);
-        soc_jprod(lamk[k] + 5, lamk[k] + 5, rsk[k] + 5);
+        const double l0 = LAM(k, 0);
+        rsk[k][0] = l0 * l0 + dss[0] * dzs_k[k][0] - sigmu;
+        double l4[4];
+        lam4(k, 1, l4);
+        soc_jprod(l4, l4, rsk[k] + 1);
+        lam4(k, 5, l4);
+        soc_jprod(l4, l4, rsk[k] + 5);
         soc_jprod(dss + 1, dzs_k[k] + 1, c1);
         soc_jprod(dss + 5, dzs_k[k] + 5, c2);
 #pragma unroll
@@ -1277,7 +1400,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     double alpha = fmin(1.0, ETA * step_len());
     // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
     // backtrack until the complementarity gap decreases
-    const bool feasible = pres < 1e-8 * nh && dres < 1e-8 * nq;
+    const bool feasible = pres < 1e-8 * NH() && dres < 1e-8 * NQ();
     for (int bt = 0; feasible && bt < 8; ++bt) {
       if (gap_at(alpha) <= gap * (1.0 - 0.01 * alpha)) break;
       alpha *= 0.5;
@@ -1316,7 +1439,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   // problems -- the rigid payload's Jl^-1 ~ 50 -- can stall at a 1e-7 gap while the structured Newton
   // solve loses accuracy; the minimiser is then still within ~1e-7 of the oracle's), otherwise
   // inaccurate (the reference holds its previous solution).
-  if (best_key < 1e300) {
+  if (BK() < 1e300) {
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -1329,7 +1452,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     }
     out.status = ST_OPTIMAL;
     out.inband = 1;
-    out.merit = best_key;
+    out.merit = BK();
   }
   return out;
 }

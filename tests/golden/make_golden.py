@@ -25,7 +25,10 @@ What each fixture pins (reference file:line):
   ref_closed_loop_sm.npz  400 ms centralized loop with the "sm" law  control/rqp_centralized.py:474-478
   ref_rp.npz          RPCentralizedController + RPDynamics closed loop control/rp_centralized.py:9-302,
                       (test/control/test_rpcentralized.py:main, 20 s)  system/rigid_payload.py:93-130
-  ref_long_<tag>.npz  rqp_example over the reference horizon (100 s; DD 10 s): f_des, iters, min_dist per HL
+  ref_c4_loop.npz     the C4 closed loop: n = 6 C-ADMM in seeded forests, 400 HL steps from near-tree starts
+                      (python -O make_golden.py c4)               control/rqp_cadmm.py:631-675,
+                                                                  example/rqp_example.py:120-131
+  ref_long_<tag>.npz  rqp_example over the reference horizon (100 s): f_des, iters, min_dist per HL
                       step, x_err / v_err per log step, states + LL wrench every 10th log step
                       (python -O make_golden.py long <controller_type>)
 """
@@ -372,7 +375,7 @@ LONG_T = {"centralized": 100.0, "consensus-admm": 100.0, "dual-decomposition": 1
 
 def gen_long_closed_loop(name, T=None, state_every=10):
     """rqp_example's main loop (example/rqp_example.py:85-131) over the reference horizon T = 100 s
-    (10 s for DD, whose reference loop takes up to 101 x 3 agent solves per step): forest seed 0,
+    (example/rqp_example.py:92, every controller type): forest seed 0,
     n = 3, HL every 10 steps, LL "pd".  Recorded per HL step: f_des, iter, min_env_dist; per log step
     (i % log_freq == 0, after that step's integrate, :114-120): x_err, v_err; and every
     ``state_every``-th log step the state and the LL wrench w = (f (n), M (3, n)).  Written to

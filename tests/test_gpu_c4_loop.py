@@ -1,0 +1,86 @@
+"""Closed-loop parity on the headline configuration: n = 6 C-ADMM in seeded
+forests over 400 HL steps (4 s) from near-tree starts, against the reference's own loop
+(ref_c4_loop.npz, tests/golden/make_golden.py gen_c4_loop: example/rqp_example.py:120-131 around
+RQPCADMMController.control, control/rqp_cadmm.py:631-675).  The GPU runs the production path --
+k_desired -> k_env_class -> k_bucket -> k_cadmm (warm state, env-class changes, the IPM start policy
+of dat_qp.hpp all interacting over hundreds of steps) -> k_rollout_agents -- for the four scenarios in
+one batch.
+
+Like the 100 s loops (test_gpu_long.py), the reference's loop reproduces itself only to a finite
+horizon: tools/c4_sensitivity.py re-runs it with the oracle QP tolerance changed 1e-11 -> 1e-10 and
+tests/golden/c4_horizon.json records, per scenario, the first HL step at which its own f_des leaves
+1e-5, its iteration count changes and its state leaves 1e-4.  The GPU must match (f_des 1e-5 relative,
+ADMM iteration counts exact, states 1e-4, min env distance 1e-4) up to that horizon and report its
+own divergence onset; beyond it both runs must stay collision-free valid closed loops.
+"""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests._golden import GOLDEN, load, unpack_flat
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _horizon():
+    p = os.path.join(GOLDEN, "c4_horizon.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+@pytest.mark.timeout(600)
+def test_gpu_c4_closed_loop_matches_reference(capsys):
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios, system
+
+    d = load("ref_c4_loop.npz")
+    n, seeds = 6, [int(s) for s in d["seeds"]]
+    S = len(seeds)
+    K = d["s0_f_des"].shape[0]
+    forests = [Forest.seeded(s) for s in seeds]
+    x0 = np.stack([system.pack_state(unpack_flat(d[f"s{k}_states"][0], n)) for k in range(S)])
+    eng = BatchedController("cadmm", n, S, scenarios.params_block(n))
+    eng.set_forests(forests, np.arange(S))
+    eng.set_state(x0, np.zeros(S, dtype=np.int32))
+    f = np.empty((S, K, 3, n))
+    its = np.empty((S, K), dtype=int)
+    md = np.empty((S, K))
+    xs = np.empty((S, K, x0.shape[1]))
+    for k in range(K):
+        xs[:, k], _ = eng.get_state()
+        r = eng.control(None, None)  # desired acceleration, env rows, C-ADMM on the device
+        f[:, k], its[:, k], md[:, k] = r.f_des, r.iters, r.min_env_dist
+        assert np.all(r.qp_status == 0)
+        eng.rollout(10)
+    assert eng.work()["inband_beyond_clarabel_tol"] == 0
+    hz = _horizon()
+    lines = []
+    for s in range(S):
+        ref_f, ref_it = d[f"s{s}_f_des"], d[f"s{s}_iters"].astype(int)
+        ref_x = np.stack([system.pack_state(unpack_flat(x, n)) for x in d[f"s{s}_states"]])
+        df = np.array([_rel(f[s, k], ref_f[k]) for k in range(K)])
+        dx = np.max(np.abs(xs[s] - ref_x), axis=1)
+        bad_f, bad_i, bad_x = df > 1e-5, its[s] != ref_it, dx > 1e-4
+        onset = [int(np.argmax(b)) if b.any() else None for b in (bad_f, bad_i, bad_x)]
+        h = hz[str(s)] if hz else {"f": K, "iters": K, "state": K}
+        Hf, Hi, Hx = (K if h[key] is None else min(K, h[key]) for key in ("f", "iters", "state"))
+        lines.append(f"scenario {s} (forest {seeds[s]}): GPU onset f_des {onset[0]}, iters {onset[1]}, state {onset[2]}; "
+                     f"reference's own horizon f_des {Hf}, iters {Hi}, state {Hx}; max f_des diff to it "
+                     f"{df[:Hf].max():.2e}; ADMM iterations {its[s].sum()} vs {ref_it.sum()}")
+        assert not bad_f[:Hf].any(), (s, int(np.argmax(bad_f)), df[:Hf].max())
+        np.testing.assert_array_equal(its[s, :Hi], ref_it[:Hi])
+        assert not bad_x[:Hx].any(), (s, int(np.argmax(bad_x)), dx[:Hx].max())
+        np.testing.assert_allclose(md[s, :Hx], d[f"s{s}_min_dist"][:Hx], rtol=0, atol=1e-4)
+        # over the whole horizon: a valid closed loop of the same controller
+        assert md[s].min() > 0.0
+        assert abs(its[s].mean() - ref_it.mean()) <= 0.25 * ref_it.mean() + 0.5
+    with capsys.disabled():
+        print("\n" + "\n".join(lines))

@@ -2,8 +2,8 @@
 
 example/rqp_example.py:main (T = 100 s, dt = 1e-3, HL every 10 steps, forest seed 0, LL "pd") run on
 the GPU by ``example.simulate_batch`` against the reference's own loop (ref_long_<tag>.npz, written
-by tests/golden/make_golden.py from the reference code): centralized and C-ADMM over the full 100 s,
-DD over 10 s (its reference loop runs up to 101 x 3 agent solves per HL step).  Every logged quantity
+by tests/golden/make_golden.py from the reference code): centralized, C-ADMM and DD (the reference's
+default controller, example/rqp_example.py:89) over the full 100 s.  Every logged quantity
 is compared (f_des_seq, iter_seq, min_env_dist_seq per HL step; x_err_seq / v_err_seq per log step;
 state_seq and w_seq every 10th log step).  north_star: closed-loop states within 1e-4 over the
 horizon; the test reports the first HL step at which f_des leaves 1e-5 or a state leaves 1e-4 (the
@@ -13,8 +13,9 @@ The reference loop is not reproducible beyond a finite horizon even against itse
 tools/long_sensitivity.py re-runs the reference's own loop (tests/golden/refstubs.py, every QP
 answered by the oracle IPM) with only the QP tolerance changed (1e-11 -> 1e-10 or 1e-12): the
 centralized loop's f_des leaves 1e-5 at HL step 3054-3055 and its states leave 1e-4 at step 3060
-(t = 30.6 s, a discrete switch of the forest CBF rows); the C-ADMM loop's f_des at step 667 (an
-ADMM iteration count flips at the 1e-2 stopping threshold) and its states at step 2280.  The GPU run is required to match (f_des 1e-5,
+(t = 30.6 s, a discrete switch of the forest CBF rows); the C-ADMM loop's f_des at step 667 and its
+states at step 2280 (its iteration counts stay identical through step 2300); the DD loop's f_des at
+step 2083, its iteration counts at step 2237 and its states at step 2240.  The GPU run is required to match (f_des 1e-5,
 iteration counts exact, states / x_err / v_err / w / min_env_dist 1e-4) up to that
 reproducibility horizon REPRO_HL (at most the recorded horizon); beyond it both runs are valid closed
 loops of the same controller and the test requires only that the GPU run completes the horizon
@@ -36,11 +37,13 @@ pytestmark = pytest.mark.gpu
 # reference's own split is at 3060); f_des to 2500 -- the GPU run meets a near-switch of the forest
 # rows at step 2543 with its state ~3e-6 away from the reference's and f_des moves by 1.1e-5 there.
 # C-ADMM: the reference's own loop (QP tol 1e-10 vs 1e-11) keeps f_des within 1e-5 only to HL step
-# 667 (an ADMM iteration count flips at the 1e-2 threshold) and its states within 1e-4 to step 2280;
-# the GPU run holds f_des to step ~2275 and its states to ~2450 (measured), and is required to within
-# the reference's own.
-REPRO_HL = {"cent": 3000, "cons": 2280, "dual": None}
-REPRO_HL_F = {"cent": 2500, "cons": 667, "dual": None}
+# 667 and its states within 1e-4 to step 2280; between the two its own f_des spread reaches 1.74e-4
+# (tools/long_sensitivity.py consensus-admm 1e-10 23), so the test's 1e-4 band there is tighter than
+# the reference's own reproducibility; the GPU run holds f_des within 1e-5 to step ~2275 and its
+# states to ~2450 (measured).  DD (tools/long_sensitivity.py dual-decomposition 1e-10 100): f_des to
+# step 2083, iteration counts to 2237, states to 2240.
+REPRO_HL = {"cent": 3000, "cons": 2280, "dual": 2240}
+REPRO_HL_F = {"cent": 2500, "cons": 667, "dual": 2083}
 
 
 def _rel(a, b):

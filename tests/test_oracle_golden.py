@@ -192,3 +192,28 @@ def test_centralized_golden():
         a = d["acc"][k]
         f, _ = ctl.control(osc.rest_state(3), (a[:3], a[3:]))
         np.testing.assert_allclose(f, d["f"][k], rtol=1e-8, atol=1e-9)
+
+
+def test_c4_closed_loop_golden():
+    """The oracle's C-ADMM + forest + dynamics reproduce the reference's n = 6 C4 closed loop
+    (ref_c4_loop.npz: control/rqp_cadmm.py:631-675 in example/rqp_example.py:120-131, seeded forests,
+    near-tree starts) over its first HL steps: f_des, ADMM iteration counts, min env distance, states."""
+    d = load("ref_c4_loop.npz")
+    n = 6
+    p = osc.params(n)
+    for s, steps in ((0, 6), (2, 4)):
+        np.random.seed(int(d["seeds"][s]))
+        forest = of.Forest()
+        ctl = oc.CADMM(p, osc.col_radius(n), forest)
+        st = unpack_flat(d[f"s{s}_states"][0], n)
+        for k in range(steps):
+            np.testing.assert_allclose(np.concatenate([st.R.reshape(-1), st.w.reshape(-1), st.xl, st.vl,
+                                                       st.Rl.reshape(-1), st.wl]), d[f"s{s}_states"][k], atol=1e-9)
+            acc, _, _ = oc.desired_acceleration_forest(st, forest)
+            f, stat = ctl.control(st, acc)
+            assert stat.iter == d[f"s{s}_iters"][k], (s, k)
+            np.testing.assert_allclose(f, d[f"s{s}_f_des"][k], rtol=1e-7, atol=1e-7)
+            assert stat.min_env_dist == pytest.approx(float(d[f"s{s}_min_dist"][k]), abs=1e-8)
+            for _ in range(10):
+                fl, M = om.low_level_control(p, st, f)
+                st.integrate(*om.forward_dynamics(p, st, fl, M), 1e-3)

@@ -71,3 +71,33 @@ __global__ __launch_bounds__(64) void probe_env(const double* prm, const double*
   }
   o[40] = e.min_env_dist + mask;
 }
+
+// ipm_solve with aux slots in the LDS row store (AUXM groups of per-iteration data out of registers)
+template <int NR, unsigned AUXM>
+__global__ __launch_bounds__(64) void probe_ipm_cadmm_aux(const double* prm, const double* lam, const double* fb,
+                                                          double* out, double* best) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  QPShared* sh = (QPShared*)smem;
+  double* env = (double*)(sh + 1);
+  double* rt = env + ENV_LDS_DOUBLES;
+  double* rows = rt + 64;
+  const int lane = threadIdx.x;
+  QPLane<1> P;
+  lane_cadmm_static(P, prm, lane % 6);
+  lane_cadmm_dynamic(P, prm, 6, lane % 6, rt, lam + 18 * lane, fb, 1.0);
+  P.emask = NR > NBASE ? 1u : 0u;
+  double y[1][3], w[6];
+  IPMOut o = ipm_solve<MODE_CADMM, 1, NR, LdsRef<QPShared>, EnvLds, RtLds, RowLds, AUXM>(
+      LdsRef<QPShared>{sh, lane / 6}, EnvLds{env, lane}, RtLds{rt, 9 * (lane % 6)}, P, prm + DAT_P_FEQ(6), y, w,
+      best + 21 * lane, 50, 1e-10, RowLds{rows, lane});
+  double* o8 = out + 16 * lane;
+  for (int c = 0; c < 3; ++c) o8[c] = y[0][c];
+  for (int c = 0; c < 6; ++c) o8[3 + c] = o.pi[c];
+  o8[9] = o.iters;
+}
+#ifndef PROBE_AUXM
+#define PROBE_AUXM 15
+#endif
+template __global__ void probe_ipm_cadmm_aux<NBASE, PROBE_AUXM>(const double*, const double*, const double*, double*, double*);
+template __global__ void probe_ipm_cadmm_aux<NBASE + 5, PROBE_AUXM>(const double*, const double*, const double*, double*, double*);
+template __global__ void probe_ipm_cadmm_aux<DAT_MAXROW, PROBE_AUXM>(const double*, const double*, const double*, double*, double*);
