@@ -54,11 +54,14 @@ def test_gpu_c4_closed_loop_matches_reference(capsys):
     its = np.empty((S, K), dtype=int)
     md = np.empty((S, K))
     xs = np.empty((S, K, x0.shape[1]))
+    # agent QPs not OPTIMAL (near-tree steps: the QP can be infeasible; the reference then holds the
+    # agent's previous solution, control/rqp_cadmm.py:496-499 -- checked through f_des below)
+    nonopt = np.zeros((S, K), dtype=int)
     for k in range(K):
         xs[:, k], _ = eng.get_state()
         r = eng.control(None, None)  # desired acceleration, env rows, C-ADMM on the device
         f[:, k], its[:, k], md[:, k] = r.f_des, r.iters, r.min_env_dist
-        assert np.all(r.qp_status == 0)
+        nonopt[:, k] = np.sum(r.qp_status != 0, axis=1)
         eng.rollout(10)
     assert eng.work()["inband_beyond_clarabel_tol"] == 0
     hz = _horizon()
@@ -74,7 +77,8 @@ def test_gpu_c4_closed_loop_matches_reference(capsys):
         Hf, Hi, Hx = (K if h[key] is None else min(K, h[key]) for key in ("f", "iters", "state"))
         lines.append(f"scenario {s} (forest {seeds[s]}): GPU onset f_des {onset[0]}, iters {onset[1]}, state {onset[2]}; "
                      f"reference's own horizon f_des {Hf}, iters {Hi}, state {Hx}; max f_des diff to it "
-                     f"{df[:Hf].max():.2e}; ADMM iterations {its[s].sum()} vs {ref_it.sum()}")
+                     f"{df[:Hf].max():.2e}; ADMM iterations {its[s].sum()} vs {ref_it.sum()}; non-optimal agent QPs "
+                     f"{nonopt[s].sum()} (steps {np.nonzero(nonopt[s])[0][:8].tolist()})")
         assert not bad_f[:Hf].any(), (s, int(np.argmax(bad_f)), df[:Hf].max())
         np.testing.assert_array_equal(its[s, :Hi], ref_it[:Hi])
         assert not bad_x[:Hx].any(), (s, int(np.argmax(bad_x)), dx[:Hx].max())
