@@ -137,7 +137,7 @@ def simulate_batch(controller_type: str, states: np.ndarray, forests: list, scen
         nxt = min(steps, (i // hl_rel_freq + 1) * hl_rel_freq, (i // log_freq + 1) * log_freq)
         eng.rollout(nxt - i)
         i = nxt
-        if progress and i % 10000 == 0:
+        if progress and i % 5000 == 0:
             print(f"t = {i * dt:.0f} s", flush=True)
     eng.close()
     return logs
