@@ -167,8 +167,11 @@ constexpr int RDS = 9;
 constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
 // G: scenario slots per wavefront (cadmm_slots)
+// doubles rounded up to a 16-byte multiple: every LDS region starts 16-byte aligned (pair reads)
+__host__ __device__ constexpr size_t al2(size_t d) { return (d + 1) & ~(size_t)1; }
 __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
-  return sizeof(double) * ((size_t)G * 12 * n) + sizeof(QPShared) * (size_t)G + sizeof(int) * 192;
+  return sizeof(double) * (al2((size_t)G * 3 * n) + (size_t)G * RT_STRIDE * n) + sizeof(QPShared) * (size_t)G +
+         sizeof(int) * 192;
 }
 __host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
   const size_t rows = lrows ? (size_t)row_lds_doubles(cadmm_nr(cls)) : 0;
@@ -206,8 +209,8 @@ struct CadmmLds {
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool lrows) {
   CadmmLds L;
   L.fbar = smem;
-  L.Rt = L.fbar + G * 3 * n;
-  L.sh = (QPShared*)(L.Rt + G * 9 * n);
+  L.Rt = L.fbar + al2(G * 3 * n);
+  L.sh = (QPShared*)(L.Rt + G * RT_STRIDE * n);
   L.done = (int*)(L.sh + G);
   L.sid = L.done + 64;
   L.wmx = L.sid + 64;
@@ -514,12 +517,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   const bool lrows = cadmm_rows_lds(n, G, CLS);  // wave-uniform
   CadmmLds L = cadmm_carve(smem, n, G, CLS, lrows);
   double* fb = L.fbar + lsc * N3;
-  double* rts = L.Rt + lsc * 9 * n;
+  double* rts = L.Rt + lsc * RT_STRIDE * n;
   double* myred = L.red + lane * RDS;
   QPShared& S = L.sh[lsc];
   const LdsRef<QPShared> shr{L.sh, lsc};
   const EnvLdsN<NE> err{L.env, lane};
-  const RtLds rtr{L.Rt, lsc * 9 * n + 9 * i};
+  const RtLds rtr{L.Rt, (lsc * n + i) * RT_STRIDE};
   if (lane < G) L.sid[lane] = -1;
   __syncthreads();
 
@@ -549,7 +552,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       sc = slot_sc;
       prm = prm_of(a, sc);
       const double* st = a.state + (size_t)sc * a.S;
-      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + 9 * i);
+      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       lam = a.clam + ((size_t)sc * n + i) * N3;
       cfs = a.cf + (size_t)sc * n * N3;
@@ -586,7 +589,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     const bool active = slot_sc >= 0;
     int it_lane = 0;
     if (active) {
-      lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho);
+      lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho, RT_STRIDE);
       P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
       double y[1][3], w[6];
       IPMOut o;
@@ -613,7 +616,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           if (j == i) {
             myf[3 * j] = y[0][0]; myf[3 * j + 1] = y[0][1]; myf[3 * j + 2] = y[0][2];
           } else {
-            cadmm_free_block(rts + 9 * j, lam + 3 * j, fb + 3 * j, o.pi, rho, myf + 3 * j);
+            cadmm_free_block(rts + RT_STRIDE * j, lam + 3 * j, fb + 3 * j, o.pi, rho, myf + 3 * j);
           }
         }
       } else if (o.status == ST_FAILED) {  // solver exception -> f_eq (control/rqp_cadmm.py:491-494)
@@ -654,7 +657,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         for (int j = 0; j < n; ++j) {
           if (j == i) continue;
           double m3[3];
-          mv3(rts + 9 * j, myf + 3 * j, m3);
+          mv3(rts + RT_STRIDE * j, myf + 3 * j, m3);
           for (int c = 0; c < 3; ++c) { F[c] += myf[3 * j + c]; M[c] += m3[c]; }
         }
         // E_F,i = F_i - (sum_k f_app_k - f_app_i), E_M,i likewise with moments of f_app
@@ -662,7 +665,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           if (k == i) continue;
           const double* fk = cfs + k * N3 + 3 * k;  // f_app_k = agent k's own block
           double m3[3];
-          mv3(rts + 9 * k, fk, m3);
+          mv3(rts + RT_STRIDE * k, fk, m3);
           for (int c = 0; c < 3; ++c) { F[c] -= fk[c]; M[c] -= m3[c]; }
         }
         for (int c = 0; c < 3; ++c) { myred[c] = F[c]; myred[3 + c] = M[c]; }
@@ -954,12 +957,12 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
   const int lsc = ls < G ? ls : 0;
-  double* X = smem;                 // NT x 9   (f_i, F_i, M_i)
-  double* lamF = X + NT * 9;        // G x 3n
-  double* lamM = lamF + G * N3;     // G x 3n
-  double* E = lamM + G * N3;        // NT x ES  consensus error (ES = 7: odd stride, no bank conflicts)
-  double* Rts = E + NT * DD_ES;     // G x 9n
-  double* red = Rts + G * 9 * n;    // 64 x DD_RS
+  double* X = smem;                     // NT x 9   (f_i, F_i, M_i)
+  double* lamF = X + al2(NT * 9);       // G x 3n
+  double* lamM = lamF + al2(G * N3);    // G x 3n
+  double* E = lamM + al2(G * N3);       // NT x ES  consensus error (ES = 7: odd stride, no bank conflicts)
+  double* Rts = E + al2(NT * DD_ES);    // G x n x RT_STRIDE
+  double* red = Rts + G * RT_STRIDE * n;  // 64 x DD_RS
   QPShared* shs = (QPShared*)(red + 64 * DD_RS);  // G
   double* envs = (double*)(shs + G);              // EnvLds image (ENV only)
   int* sid = (int*)(envs + dd_area_doubles(ENV));  // G: scenario of the slot (-1 empty, -2 retired)
@@ -968,11 +971,11 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* myX = X + lane * 9;
   double* lF = lamF + lsc * N3;
   double* lM = lamM + lsc * N3;
-  double* rts = Rts + lsc * 9 * n;
+  double* rts = Rts + lsc * RT_STRIDE * n;
   const int cnt = a.scount[0], first = a.scount[NCLS];
   const LdsRef<QPShared> shr{shs, lsc};
   const EnvLds err{envs, lane};
-  const RtLds rtr{Rts, lsc * 9 * n + 9 * i};
+  const RtLds rtr{Rts, (lsc * n + i) * RT_STRIDE};
   if (lane < G) sid[lane] = -1;
   __syncthreads();
 
@@ -999,7 +1002,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       prm = prm_of(a, sc);
       const double* st = a.state + (size_t)sc * a.S;
       Rl = st + DAT_S_RL(n);
-      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, Rl, rts + 9 * i);
+      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, Rl, rts + RT_STRIDE * i);
       for (int c = 0; c < 3; ++c) {
         lF[3 * i + c] = a.dlamF[(size_t)sc * N3 + 3 * i + c];
         lM[3 * i + c] = a.dlamM[(size_t)sc * N3 + 3 * i + c];
@@ -1091,7 +1094,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         if (k == i) continue;
         const double* fk = X + (ls * n + k) * 9;
         double m3[3];
-        mv3(rts + 9 * k, fk, m3);
+        mv3(rts + RT_STRIDE * k, fk, m3);
         for (int c = 0; c < 3; ++c) { sf[c] += fk[c]; sm[c] += m3[c]; }
       }
       for (int c = 0; c < 3; ++c) {
@@ -1685,7 +1688,8 @@ KArgs kargs(dat_handle* h) {
 
 size_t dd_lds(int n, bool env) {
   int G = 64 / n, NT = G * n;
-  return sizeof(double) * ((size_t)NT * 9 + 2 * (size_t)G * 3 * n + (size_t)NT * DD_ES + (size_t)G * 9 * n + 64 * DD_RS) +
+  return sizeof(double) * (al2((size_t)NT * 9) + 2 * al2((size_t)G * 3 * n) + al2((size_t)NT * DD_ES) +
+                           (size_t)G * RT_STRIDE * n + 64 * DD_RS) +
          sizeof(QPShared) * (size_t)G + sizeof(double) * dd_area_doubles(env) + sizeof(int) * 128;
 }
 size_t dd_setup_lds(int n) {

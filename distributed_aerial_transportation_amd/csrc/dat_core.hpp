@@ -33,20 +33,54 @@ enum Mode { MODE_CENT = 0, MODE_CADMM = 1, MODE_DD = 2 };
 // =====================================================================================
 // small linear algebra (row-major)
 // =====================================================================================
+// LDS address space: solver data kept in LDS is read through volatile address_space(3) pointers
+// (dat_qp.hpp "How the IPM reads LDS").
+#define DAT_LDS __attribute__((address_space(3)))
+typedef double dat_d2 __attribute__((ext_vector_type(2)));
+
+// N consecutive doubles into registers.  Plain pointers: element copies.  A volatile LDS pointer to
+// a 16-byte aligned record: one ds_read_b128 per pair -- the compiler never merges volatile reads,
+// so element reads would be N ds_read_b64 instructions, each with its own wait (every LDS-resident
+// record the kernels read this way starts on a 16-byte boundary: QPShared, the RT_STRIDE U-maps).
+template <int N, class P>
+DAT_HD void ldn(P p, double* o) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) o[k] = p[k];
+}
+template <int N>
+DAT_HD void ldn(const volatile DAT_LDS double* p, double* o) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const volatile DAT_LDS dat_d2* q = (const volatile DAT_LDS dat_d2*)p;
+#pragma unroll
+  for (int k = 0; k < N / 2; ++k) {
+    const dat_d2 v = q[k];
+    o[2 * k] = v.x;
+    o[2 * k + 1] = v.y;
+  }
+  if (N & 1) o[N - 1] = p[N - 1];
+#else
+  for (int k = 0; k < N; ++k) o[k] = p[k];
+#endif
+}
+
 DAT_HD double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 DAT_HD void cross3(const double* a, const double* b, double* o) {
   double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
 }
 template <class PM>
-DAT_HD void mv3(PM M, const double* v, double* o) {
+DAT_HD void mv3(PM Mp, const double* v, double* o) {
+  double M[9];
+  ldn<9>(Mp, M);
   double x = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
   double y = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
   double z = M[6] * v[0] + M[7] * v[1] + M[8] * v[2];
   o[0] = x; o[1] = y; o[2] = z;
 }
 template <class PM>
-DAT_HD void mtv3(PM M, const double* v, double* o) {
+DAT_HD void mtv3(PM Mp, const double* v, double* o) {
+  double M[9];
+  ldn<9>(Mp, M);
   double x = M[0] * v[0] + M[3] * v[1] + M[6] * v[2];
   double y = M[1] * v[0] + M[4] * v[1] + M[7] * v[2];
   double z = M[2] * v[0] + M[5] * v[1] + M[8] * v[2];
@@ -132,8 +166,7 @@ DAT_HD constexpr int sp3(int r, int c) {
 template <class PA>
 DAT_HD void spmv6(PA Ap, const double* v, double* o) {
   double A[21];
-#pragma unroll
-  for (int k = 0; k < 21; ++k) A[k] = Ap[k];  // one read per entry (Ap may be a volatile LDS pointer)
+  ldn<21>(Ap, A);  // one read per entry pair (Ap may be a volatile LDS pointer)
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     double s = 0.0;
@@ -305,8 +338,7 @@ template <class PR>
 DAT_HD void add_UDUt(double* M, PR Rtp, const double* D, double scale) {
   double Df[9] = {D[0], D[1], D[2], D[1], D[3], D[4], D[2], D[4], D[5]};
   double Rt[9], RD[9], RDR[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) Rt[k] = Rtp[k];  // one read per entry (Rtp may be a volatile LDS pointer)
+  ldn<9>(Rtp, Rt);  // one read per entry pair (Rtp may be a volatile LDS pointer)
   mm3(Rt, Df, RD);
   mmt3(RD, Rt, RDR);
 #pragma unroll

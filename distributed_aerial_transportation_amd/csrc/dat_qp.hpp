@@ -60,16 +60,24 @@ constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton so
 #define DAT_IPM_REFINE_MODE 1
 #endif
 
-struct QPShared {
-  double inv_mT, Bv[9], JTi[9], bv[3], bw[3];
-  double C[2][21];     // packed u-space Hessian: [0] without, [1] with the leader's desired-acc terms
-  double cu[2][6];     // matching linear terms
-  double K[21];        // C-ADMM: sum over ALL agents of U_j U_j' (agent i subtracts its own term)
-  double ba[NBASE][3]; // base rows: coefficients on dwl (slots 0, 1) or dvl (slot 2)
-  double bb[NBASE];    // constants (the affine offsets bw / bv folded in)
-  int bmask;           // active base slots
-  int infeasible;      // a dropped all-zero row had a negative constant
+// Every array starts on a 16-byte boundary and the kernels place the record 16-byte aligned in LDS,
+// so the solver reads entry pairs (ldn: one ds_read_b128 per pair).
+struct alignas(16) QPShared {
+  double C[2][22];       // packed u-space Hessian (21 + pad): [0] without, [1] with the leader's desired-acc terms
+  double K[22];          // C-ADMM: sum over ALL agents of U_j U_j' (agent i subtracts its own term)
+  double cu[2][6];       // matching linear terms
+  double Bv[10], JTi[10];  // 3x3 row-major + pad
+  double rows[NBASE][4]; // base rows (a0, a1, a2, b): coefficients on dwl (slots 0, 1) or dvl (slot 2) and
+                         // the constant (the affine offsets bw / bv folded in)
+  double bv[4], bw[4];
+  double inv_mT, pad_;
+  int bmask;             // active base slots
+  int infeasible;        // a dropped all-zero row had a negative constant
+  int pad2_[2];
 };
+// LDS stride (doubles) of the U-maps Rt_j the C-ADMM / DD kernels keep per agent: 9 + pad, so each
+// map starts on a 16-byte boundary (ldn pair reads)
+constexpr int RT_STRIDE = 10;
 
 // env CBF rows of one agent (dvl): a . lin_v(u) + b >= 0 (kept in LDS by the kernels)
 struct EnvRows {
@@ -89,7 +97,6 @@ struct PlainRef {
 // solver loops: every use is a ds_read with an immediate offset at the point of use (the compiler
 // may not hoist, merge or cache a volatile load), costing no register between uses and no address
 // arithmetic.
-#define DAT_LDS __attribute__((address_space(3)))
 template <class T>
 __device__ inline const DAT_LDS T* lds_opaque(const DAT_LDS T* p) {
 #ifndef DAT_LDS_HOIST
@@ -111,27 +118,28 @@ struct EnvPlain {
   DAT_HD void a3(int j, double* o) const { o[0] = p->a[j][0]; o[1] = p->a[j][1]; o[2] = p->a[j][2]; }
   DAT_HD void ab(int j, double* o, double& bb) const { a3(j, o); bb = p->b[j]; }
 };
-// LDS image of the env rows of a 64-lane wavefront, structure of arrays so that the lanes of a
-// wavefront reading the same slot hit 64 consecutive doubles (bank-conflict free; a per-lane
-// struct with its 40-double stride maps 32 lanes onto 4 banks), NE env slots:
-//   a_j[c] of lane l at [(3 j + c) * 64 + l],  b_j at [(3 NE + j) * 64 + l].
+// LDS image of the env rows of a 64-lane wavefront, pairs structure of arrays: env slot j is two
+// pair fields, (a_j0, a_j1) and (a_j2, b_j), each 64 lanes x 16 bytes, so a lane reads a row with two
+// ds_read_b128 and a wavefront reading one field touches 1 KB of consecutive LDS (conflict free):
+//   field 2 j + h of lane l at doubles [(2 j + h) * 128 + 2 l, +1].
 __host__ __device__ constexpr int env_lds_doubles(int NE) { return 4 * NE * 64; }
 constexpr int ENV_LDS_DOUBLES = env_lds_doubles(DAT_NENV);
+DAT_HD constexpr int env_lds_index(int j, int c, int lane) { return (2 * j + (c >> 1)) * 128 + 2 * lane + (c & 1); }
 template <int NE>
 struct EnvLdsN {
-  const DAT_LDS double* p;  // the lane's column
-  __device__ EnvLdsN(const double* b, int lane) : p((const DAT_LDS double*)(b + lane)) {}
-  __device__ const DAT_LDS double* col() const { return lds_opaque(p); }
-  __device__ double a(int j, int c) const { return ((const volatile DAT_LDS double*)p)[(3 * j + c) * 64]; }
-  __device__ double b(int j) const { return ((const volatile DAT_LDS double*)p)[(3 * NE + j) * 64]; }
-  // one opaque offset for the row's coefficients (and constant)
+  const DAT_LDS double* p;  // the lane's pair column
+  __device__ EnvLdsN(const double* b, int lane) : p((const DAT_LDS double*)(b + 2 * lane)) {}
+  __device__ dat_d2 field(int f) const { return ((const volatile DAT_LDS dat_d2*)p)[f * 64]; }
+  __device__ double a(int j, int c) const { return ((const volatile DAT_LDS double*)p)[env_lds_index(j, c, 0)]; }
+  __device__ double b(int j) const { return ((const volatile DAT_LDS double*)p)[env_lds_index(j, 3, 0)]; }
   __device__ void a3(int j, double* o) const {
-    o[0] = a(j, 0); o[1] = a(j, 1); o[2] = a(j, 2);
+    const dat_d2 f0 = field(2 * j), f1 = field(2 * j + 1);
+    o[0] = f0.x; o[1] = f0.y; o[2] = f1.x;
   }
   __device__ void ab(int j, double* o, double& bb) const {
-    const volatile DAT_LDS double* q = p;
-    o[0] = q[(3 * j) * 64]; o[1] = q[(3 * j + 1) * 64]; o[2] = q[(3 * j + 2) * 64];
-    bb = q[(3 * NE + j) * 64];
+    const dat_d2 f0 = field(2 * j), f1 = field(2 * j + 1);
+    o[0] = f0.x; o[1] = f0.y; o[2] = f1.x;
+    bb = f1.y;
   }
 };
 using EnvLds = EnvLdsN<DAT_NENV>;
@@ -141,8 +149,8 @@ DAT_HD void env_to_lds(double* base, int lane, const EnvRows& E) {
 #pragma unroll
   for (int j = 0; j < NE; ++j) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) base[(3 * j + c) * 64 + lane] = E.a[j][c];
-    base[(3 * NE + j) * 64 + lane] = E.b[j];
+    for (int c = 0; c < 3; ++c) base[env_lds_index(j, c, lane)] = E.a[j][c];
+    base[env_lds_index(j, 3, lane)] = E.b[j];
   }
 }
 
@@ -154,7 +162,7 @@ struct RtPtr {
 struct RtLds {
   const volatile DAT_LDS double* p;  // block 0
   __device__ RtLds(const double* b, int off) : p((const volatile DAT_LDS double*)(b + off)) {}
-  __device__ const volatile DAT_LDS double* get(int k) const { return p + 9 * k; }
+  __device__ const volatile DAT_LDS double* get(int k) const { return p + RT_STRIDE * k; }
 };
 
 template <int NB>
@@ -208,6 +216,9 @@ DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st
   bv[1] = -t1[1] + t2[1];
   bv[2] = -DAT_GRAVITY - t1[2] + t2[2];
   for (int c = 0; c < 3; ++c) { S.bw[c] = bw[c]; S.bv[c] = bv[c]; }
+  S.bw[3] = S.bv[3] = 0.0;
+  S.Bv[9] = S.JTi[9] = 0.0;
+  S.pad_ = 0.0;
 
   // Phi(u) = k_f ||S - mT g e3||^2 + k_m ||Mo||^2 + kdv (||dvl||^2 - 2 dvl_des'dvl)
   //          + kdv (||dwl||^2 - 2 dwl_des'dwl)          (control/rqp_cadmm.py:436-458)
@@ -215,7 +226,7 @@ DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st
     if (!((variants >> v) & 1)) continue;
     double* C = S.C[v];
     double* cu = S.cu[v];
-    for (int k = 0; k < 21; ++k) C[k] = 0.0;
+    for (int k = 0; k < 22; ++k) C[k] = 0.0;
     for (int r = 0; r < 3; ++r) { C[sp6(r, r)] = 2.0 * k_f; C[sp6(3 + r, 3 + r)] = 2.0 * k_m; }
     for (int r = 0; r < 6; ++r) cu[r] = 0.0;
     cu[2] = -2.0 * k_f * mT * DAT_GRAVITY;
@@ -244,7 +255,7 @@ DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st
     }
   }
   if (with_K) {
-    for (int k = 0; k < 21; ++k) S.K[k] = 0.0;
+    for (int k = 0; k < 22; ++k) S.K[k] = 0.0;
     const double I3[6] = {1, 0, 0, 1, 0, 1};
     for (int j = 0; j < n; ++j) {
       double Rt[9];
@@ -266,13 +277,13 @@ DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st
   double beta[NBASE] = {dot3(Rl + 6, b) + 2.0 * dot3(Rl + 6, a) + (Rl[8] - prm[DAT_P_COSP]),
                         prm[DAT_P_MAXWL2] - dot3(wl, wl), prm[DAT_P_MAXVL2] - dot3(vl, vl)};
   for (int l = 0; l < NBASE; ++l) {
-    for (int c = 0; c < 3; ++c) S.ba[l][c] = al[l][c];
+    for (int c = 0; c < 3; ++c) S.rows[l][c] = al[l][c];
     if (al[l][0] == 0.0 && al[l][1] == 0.0 && al[l][2] == 0.0) {
       if (beta[l] < 0.0) S.infeasible = 1;  // 0 >= -beta fails: the QP is infeasible
-      S.bb[l] = 1.0;                        // 0 >= 0 carries no information: padding row
+      S.rows[l][3] = 1.0;                   // 0 >= 0 carries no information: padding row
       continue;
     }
-    S.bb[l] = beta[l] + dot3(al[l], l < NWROW ? bw : bv);
+    S.rows[l][3] = beta[l] + dot3(al[l], l < NWROW ? bw : bv);
     S.bmask |= 1 << l;
   }
 }
@@ -336,7 +347,7 @@ DAT_HD void lane_cadmm_static(QPLane<1>& P, const double* prm, int i) {
 // per-iteration part: penalty rho and a = fbar - lam / rho.  lam, fbar: (3n) agent-major;
 // Rt_all: n x 9.
 DAT_HD void lane_cadmm_dynamic(QPLane<1>& P, const double* prm, int n, int i, const double* Rt_all,
-                               const double* lam, const double* fbar, double rho) {
+                               const double* lam, const double* fbar, double rho, int rt_stride = 9) {
   const double kfeq = prm[DAT_P_KFEQ];
   const double irho = 1.0 / rho;
   P.rho = rho;
@@ -352,7 +363,7 @@ DAT_HD void lane_cadmm_dynamic(QPLane<1>& P, const double* prm, int n, int i, co
       for (int c = 0; c < 3; ++c) P.q[0][c] = -2.0 * kfeq * feq[c] - rho * a[c];
     } else {
       double t[6];
-      U_apply(Rt_all + 9 * j, a, t);
+      U_apply(Rt_all + rt_stride * j, a, t);
 #pragma unroll
       for (int r = 0; r < 6; ++r) P.atil[r] += t[r];
     }
@@ -481,12 +492,12 @@ DAT_HD double soc_step(const double* x, const double* d) {
 }
 
 // Per-row IPM state (slack s_l, dual z_l, Newton row term zw_l of each row slot).  RowRegs keeps
-// it in registers; RowLds in a structure-of-arrays LDS image over the 64 lanes of a wavefront
-// (slot l of lane j: s at [l 64 + j], z at [(NR + l) 64 + j], zw at [(2 NR + l) 64 + j]; a
-// wavefront reading one slot touches 64 consecutive doubles, bank-conflict free), read and written
-// through an index the compiler cannot see through, so the rows cost no registers between uses.
-// Besides the rows, a store may hold NX auxiliary per-lane doubles (aux slots: the per-iteration
-// quantities ipm_solve's AUXM mask moves out of the register file, see ipm_aux_doubles).
+// it in registers; RowLds in an LDS image over the 64 lanes of a wavefront: the (s_l, z_l) pair of
+// slot l of lane j at doubles [l 128 + 2 j, +1] (one ds_read_b128 / ds_write_b128 per pair; a
+// wavefront touches 1 KB of consecutive LDS), zw_l at [2 NR 64 + l 64 + j]; read and written through
+// volatile pointers, so the rows cost no registers between uses.  Besides the rows, a store may hold
+// NX auxiliary per-lane doubles at [(3 NR + k) 64 + j] (aux slots: the per-iteration quantities
+// ipm_solve's AUXM mask moves out of the register file, see ipm_aux_doubles).
 struct RowRegs {
   template <int NR, int NX = 0>
   struct Store {
@@ -496,6 +507,8 @@ struct RowRegs {
     DAT_HD double& z(int l) { return z_[l]; }
     DAT_HD double& w(int l) { return w_[l]; }
     DAT_HD double& x(int k) { return x_[k]; }
+    DAT_HD void sz(int l, double& sv, double& zv) { sv = s_[l]; zv = z_[l]; }
+    DAT_HD void set_sz(int l, double sv, double zv) { s_[l] = sv; z_[l] = zv; }
   };
 };
 struct RowLds {
@@ -503,16 +516,29 @@ struct RowLds {
   int lane;
   template <int NR, int NX = 0>
   struct Store {
-    DAT_LDS double* p;  // the lane's column
-    __device__ explicit Store(const RowLds& r) : p((DAT_LDS double*)(r.base + r.lane)) {}
+    DAT_LDS double* p;   // the lane's zw / aux column
+    DAT_LDS double* pz;  // the lane's (s, z) pair column
+    __device__ explicit Store(const RowLds& r)
+        : p((DAT_LDS double*)(r.base + r.lane)), pz((DAT_LDS double*)(r.base + 2 * r.lane)) {}
     __device__ volatile DAT_LDS double& at(int k) { return ((volatile DAT_LDS double*)p)[k * 64]; }
-    __device__ volatile DAT_LDS double& s(int l) { return at(l); }
-    __device__ volatile DAT_LDS double& z(int l) { return at(NR + l); }
+    __device__ volatile DAT_LDS double& s(int l) { return ((volatile DAT_LDS double*)pz)[l * 128]; }
+    __device__ volatile DAT_LDS double& z(int l) { return ((volatile DAT_LDS double*)pz)[l * 128 + 1]; }
     __device__ volatile DAT_LDS double& w(int l) { return at(2 * NR + l); }
     __device__ volatile DAT_LDS double& x(int k) { return at(3 * NR + k); }
+    __device__ void sz(int l, double& sv, double& zv) {
+      const dat_d2 v = ((volatile DAT_LDS dat_d2*)pz)[l * 64];
+      sv = v.x;
+      zv = v.y;
+    }
+    __device__ void set_sz(int l, double sv, double zv) {
+      dat_d2 v;
+      v.x = sv;
+      v.y = zv;
+      ((volatile DAT_LDS dat_d2*)pz)[l * 64] = v;
+    }
   };
 };
-// Host model of RowLds (the same strided column in ordinary memory): exercises the aux / row store
+// Host model of RowLds (the same strided columns in ordinary memory): exercises the aux / row store
 // code paths of ipm_solve in the host build (tests/hostsim).
 struct RowMem {
   double* base;
@@ -520,12 +546,15 @@ struct RowMem {
   template <int NR, int NX = 0>
   struct Store {
     double* p;
-    DAT_HD explicit Store(const RowMem& r) : p(r.base + r.lane) {}
+    double* pz;
+    DAT_HD explicit Store(const RowMem& r) : p(r.base + r.lane), pz(r.base + 2 * r.lane) {}
     DAT_HD double& at(int k) { return p[k * 64]; }
-    DAT_HD double& s(int l) { return at(l); }
-    DAT_HD double& z(int l) { return at(NR + l); }
+    DAT_HD double& s(int l) { return pz[l * 128]; }
+    DAT_HD double& z(int l) { return pz[l * 128 + 1]; }
     DAT_HD double& w(int l) { return at(2 * NR + l); }
     DAT_HD double& x(int k) { return at(3 * NR + k); }
+    DAT_HD void sz(int l, double& sv, double& zv) { sv = s(l); zv = z(l); }
+    DAT_HD void set_sz(int l, double sv, double zv) { s(l) = sv; z(l) = zv; }
   };
 };
 // aux slots of ipm_solve (AUXM bits): SCAL the stopping-rule scales and best merits (4), RES the
@@ -536,7 +565,7 @@ __host__ __device__ constexpr int ipm_aux_doubles(int NB, unsigned AUXM) {
   return ((AUXM & AUX_SCAL) ? 4 : 0) + ((AUXM & AUX_RES) ? 3 * NB + 6 : 0) + ((AUXM & AUX_LAM) ? 9 * NB : 0) +
          ((AUXM & AUX_DINV) ? 7 * NB : 0);
 }
-__host__ __device__ constexpr int row_lds_doubles(int NR, int NX = 0) { return (3 * NR + NX) * 64; }
+__host__ __device__ constexpr int row_lds_doubles(int NR, int NX = 0) { return (3 * NR + NX) * 64; }  // (s, z) pairs, zw, aux
 
 struct IPMOut {
   int status;
@@ -596,15 +625,13 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   auto act = [&](int l) -> double { return ((mask >> l) & 1u) ? 1.0 : 0.0; };
   auto Cp = [&]() { return &sh.get().C[var][0]; };
   auto cup = [&]() { return &sh.get().cu[var][0]; };
-  auto ra = [&](int l, int c) -> double {
-    return l < NBASE ? sh.get().ba[l < NBASE ? l : 0][c] : er.a(l >= NBASE ? l - NBASE : 0, c);
-  };
-  auto rb = [&](int l) -> double { return l < NBASE ? sh.get().bb[l < NBASE ? l : 0] : er.b(l >= NBASE ? l - NBASE : 0); };
-  // row coefficients a_l (one opaque access per row)
+  auto rb = [&](int l) -> double { return l < NBASE ? sh.get().rows[l < NBASE ? l : 0][3] : er.b(l >= NBASE ? l - NBASE : 0); };
+  // row coefficients a_l (base rows: two pair reads of the (a, b) record)
   auto ra3 = [&](int l, double* a) {
     if (l < NBASE) {
-      const int b = l < NBASE ? l : 0;
-      a[0] = sh.get().ba[b][0]; a[1] = sh.get().ba[b][1]; a[2] = sh.get().ba[b][2];
+      double r4[4];
+      ldn<4>(sh.get().rows[l < NBASE ? l : 0], r4);
+      a[0] = r4[0]; a[1] = r4[1]; a[2] = r4[2];
     } else {
       er.a3(l >= NBASE ? l - NBASE : 0, a);
     }
@@ -621,10 +648,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     const double* x = l < NWROW ? dw : dv;
     double a[3], b;
     if (l < NBASE) {
-      const auto& S = sh.get();
-      const int k = l < NBASE ? l : 0;
-      a[0] = S.ba[k][0]; a[1] = S.ba[k][1]; a[2] = S.ba[k][2];
-      b = S.bb[k];
+      double r4[4];
+      ldn<4>(sh.get().rows[l < NBASE ? l : 0], r4);
+      a[0] = r4[0]; a[1] = r4[1]; a[2] = r4[2];
+      b = r4[3];
     } else {
       er.ab(l >= NBASE ? l - NBASE : 0, a, b);
     }
@@ -771,7 +798,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     zk[k][0] = Z0; zk[k][1] = Z0; zk[k][5] = Z0;
   }
 #pragma unroll
-  for (int l = 0; l < NR; ++l) ZL(l) = Z0 * act(l);
+  for (int l = 0; l < NR; ++l) ZL(l) = Z0 * act(l);  // (the slack half of the pair is written below)
 #pragma unroll
   for (int r = 0; r < 6; ++r) w[r] = 0.0;
   // C-ADMM: the free aggregate starts at its unconstrained minimiser without the u-coupling,
@@ -822,8 +849,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       lin(u, dv, dw);
       spmv6(Cp(), u, pi);
       rows_adj(ZL, az);
+      {
+        double cu6[6];
+        ldn<6>(cup(), cu6);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) pi[r] += cup()[r] - az[r];
+        for (int r = 0; r < 6; ++r) pi[r] += cu6[r] - az[r];
+      }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         double ut[3], gz[3];
@@ -871,10 +902,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        const double rl = SL(l) - (rowval(l, dv, dw));
+        double sl, zl;
+        rst.sz(l, sl, zl);
+        const double rl = sl - (rowval(l, dv, dw));
         pres = fmax(pres, fabs(rl));
         chk += rl;
-        gap += SL(l) * ZL(l);
+        gap += sl * zl;
       }
       out.iters = it;
       if (!(fabs(chk + gap) < 1e300)) {  // NaN or Inf anywhere in the residuals
@@ -997,7 +1030,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         double Xv[6] = {0, 0, 0, 0, 0, 0}, Xw[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int l = 0; l < NR; ++l) {
-          const double wgt = ZL(l) * frcp(SL(l));
+          double sl, zl;
+          rst.sz(l, sl, zl);
+          const double wgt = zl * frcp(sl);
           double* X = l < NWROW ? Xw : Xv;
           double a3v[3];
           ra3(l, a3v);
@@ -1007,15 +1042,18 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         }
         // Av = [im I, Bv];  Av' Xv Av = [[im^2 Xv, im Xv Bv], [., Bv' Xv Bv]];  Aw = [0, JTi]
         const auto& S = sh.get();
-        double XB[9], XJ[9];
+        double XB[9], XJ[9], Bv[10], JTi[10];
+        ldn<10>(S.Bv, Bv);
+        ldn<10>(S.JTi, JTi);
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            XB[3 * r + c] = Xv[sp3(r, 0)] * S.Bv[c] + Xv[sp3(r, 1)] * S.Bv[3 + c] + Xv[sp3(r, 2)] * S.Bv[6 + c];
-            XJ[3 * r + c] = Xw[sp3(r, 0)] * S.JTi[c] + Xw[sp3(r, 1)] * S.JTi[3 + c] + Xw[sp3(r, 2)] * S.JTi[6 + c];
+            XB[3 * r + c] = Xv[sp3(r, 0)] * Bv[c] + Xv[sp3(r, 1)] * Bv[3 + c] + Xv[sp3(r, 2)] * Bv[6 + c];
+            XJ[3 * r + c] = Xw[sp3(r, 0)] * JTi[c] + Xw[sp3(r, 1)] * JTi[3 + c] + Xw[sp3(r, 2)] * JTi[6 + c];
           }
-        const auto* C = &S.C[var][0];
+        double C[22];
+        ldn<22>(&S.C[var][0], C);
 #pragma unroll
         for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -1024,7 +1062,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
               Mm[sp6(r, c)] = C[sp6(r, c)] + im * im * Xv[sp3(r, c)];
               double s = C[sp6(3 + r, 3 + c)];
 #pragma unroll
-              for (int k2 = 0; k2 < 3; ++k2) s += S.Bv[3 * k2 + r] * XB[3 * k2 + c] + S.JTi[3 * k2 + r] * XJ[3 * k2 + c];
+              for (int k2 = 0; k2 < 3; ++k2) s += Bv[3 * k2 + r] * XB[3 * k2 + c] + JTi[3 * k2 + r] * XJ[3 * k2 + c];
               Mm[sp6(3 + r, 3 + c)] = s;
             }
             Mm[sp6(r, 3 + c)] = C[sp6(r, 3 + c)] + im * XB[3 * r + c];
@@ -1043,7 +1081,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         // T = sum_k U_k D_k^-1 U_k' (+ K_{-i} / rho)
         double T[21];
         if (MODE == MODE_CADMM) {
-          const auto* K = &sh.get().K[0];
+          double K[22];
+          ldn<22>(&sh.get().K[0], K);
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
           // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
@@ -1201,14 +1240,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        const double is = frcp(SL(l));
-        const double rzl = SL(l) - (rowval(l, dv, dw));
+        double sl, zl;
+        rst.sz(l, sl, zl);
+        const double is = frcp(sl);
+        const double rzl = sl - (rowval(l, dv, dw));
         double cadd = 0.0;
         if (corr) {
           const double a = rowdot(l, ddva, ddwa);
-          cadd = act(l) * ((-rzl + a) * (ZW(l) - ZL(l) * is * a) - sigmu);
+          cadd = act(l) * ((-rzl + a) * (ZW(l) - zl * is * a) - sigmu);
         }
-        ZW(l) = (ZL(l) * rzl - (SL(l) * ZL(l) + cadd)) * is;
+        ZW(l) = (zl * rzl - (sl * zl + cadd)) * is;
       }
       rows_adj(ZW, bu);
       {
@@ -1238,7 +1279,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0}, adz[6];
 #pragma unroll
           for (int l = 0; l < NR; ++l) {
-            const double dzl = ZW(l) - ZL(l) * frcp(SL(l)) * rowdot(l, ddv, ddw);
+            double sl, zl;
+            rst.sz(l, sl, zl);
+            const double dzl = ZW(l) - zl * frcp(sl) * rowdot(l, ddv, ddw);
             double* g = l < NWROW ? gw : gv;
             double a[3];
             ra3(l, a);
@@ -1296,10 +1339,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
     };
     // row directions of the current Newton solution
-    auto row_dirs = [&](int l, const double* ddv, const double* ddw, double& ds, double& dz) {
+    // (s_l, z_l) of the row: sl, zl (one pair read by the caller)
+    auto row_dirs = [&](int l, const double* ddv, const double* ddw, double sl, double zl, double& ds, double& dz) {
       const double a = rowdot(l, ddv, ddw);
-      ds = -(SL(l) - (rowval(l, dv, dw))) + a;
-      dz = ZW(l) - ZL(l) * frcp(SL(l)) * a;
+      ds = -(sl - (rowval(l, dv, dw))) + a;
+      dz = ZW(l) - zl * frcp(sl) * a;
     };
     auto step_len = [&]() {
       double a = 1e300;
@@ -1324,9 +1368,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
-        row_dirs(l, ddv, ddw, ds, dz);
-        if (ds < 0) a = fmin(a, -SL(l) * frcp(ds));
-        if (dz < 0) a = fmin(a, -ZL(l) * frcp(dz));
+        double sl, zl;
+        rst.sz(l, sl, zl);
+        row_dirs(l, ddv, ddw, sl, zl, ds, dz);
+        if (ds < 0) a = fmin(a, -sl * frcp(ds));
+        if (dz < 0) a = fmin(a, -zl * frcp(dz));
       }
       return a;
     };
@@ -1345,8 +1391,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
-        row_dirs(l, ddv, ddw, ds, dz);
-        g += (SL(l) + al * ds) * (ZL(l) + al * dz);
+        double sl, zl;
+        rst.sz(l, sl, zl);
+        row_dirs(l, ddv, ddw, sl, zl, ds, dz);
+        g += (sl + al * ds) * (zl + al * dz);
       }
       return g;
     };
@@ -1428,9 +1476,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
-        row_dirs(l, ddv, ddw, ds, dz);
-        SL(l) += alpha * ds;
-        ZL(l) += alpha * dz;
+        double sl, zl;
+        rst.sz(l, sl, zl);
+        row_dirs(l, ddv, ddw, sl, zl, ds, dz);
+        rst.set_sz(l, sl + alpha * ds, zl + alpha * dz);
       }
     }
   }
