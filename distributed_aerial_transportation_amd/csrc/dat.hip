@@ -173,27 +173,50 @@ __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
   return sizeof(double) * (al2((size_t)G * 3 * n) + (size_t)G * RT_STRIDE * n) + sizeof(QPShared) * (size_t)G +
          sizeof(int) * 192;
 }
-__host__ __device__ inline size_t cadmm_area_doubles(int cls, bool lrows) {
-  const size_t rows = lrows ? (size_t)row_lds_doubles(cadmm_nr(cls)) : 0;
+// IPM per-iteration quantities moved to LDS aux slots (ipm_solve AUXM) per env class, when the class's
+// carve still fits the budget: class 0 all groups (its 3 row slots leave room; class-0 probe scratch
+// traffic 145 -> 23 ops per IPM pass; A/B on MI355X: C2 12.1 -> 11.0 ms, C5 80.7 -> 73.2 ms per step);
+// classes 1 and 2 none (lambda alone in class 1: C4 3.66 vs 3.67 ms, no gain; class 2's 5 env rows
+// fill the budget).
+#ifndef DAT_AUXM0
+#define DAT_AUXM0 15
+#endif
+#ifndef DAT_AUXM1
+#define DAT_AUXM1 0
+#endif
+#ifndef DAT_AUXM2
+#define DAT_AUXM2 0
+#endif
+__host__ __device__ constexpr unsigned cadmm_auxm(int cls) {
+  return cls == 0 ? DAT_AUXM0 : cls == 1 ? DAT_AUXM1 : cls == 2 ? DAT_AUXM2 : 0u;
+}
+// row-state placement of a class: 0 registers, 1 LDS rows, 2 LDS rows + aux slots
+__host__ __device__ inline size_t cadmm_area_doubles(int cls, int rmode) {
+  const size_t rows = rmode ? (size_t)row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
   return (rows > 64 * RDS ? rows : 64 * RDS) + (size_t)env_lds_doubles(class_env_rows(cls));
 }
-// row state of class cls in LDS: classes ROWLDS_MIN_CLS .. 2 when the image fits the budget; class 3
-// (13 slots) never.  Few row slots are cheaper in registers: an LDS row access costs a register
-// copy and an LDS round trip, which pays only once the rows would otherwise spill.
+// row state of class cls in LDS: with the class's aux slots when that carve fits the budget, else rows
+// alone for classes ROWLDS_MIN_CLS .. 2; class 3 (13 slots) never.  Few row slots without aux slots
+// are cheaper in registers: an LDS row access costs an LDS round trip, which pays only once the rows
+// would otherwise spill.
 #ifndef DAT_ROWLDS_MIN_CLS
 #define DAT_ROWLDS_MIN_CLS 1
 #endif
 constexpr int ROWLDS_MIN_CLS = DAT_ROWLDS_MIN_CLS;
-__host__ __device__ inline bool cadmm_rows_lds(int n, int G, int cls) {
-  if (cls >= NCLS - 1 || cls < ROWLDS_MIN_CLS) return false;
-  return cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, true) <= LDS_WAVE_BUDGET;
+__host__ __device__ inline int cadmm_row_mode(int n, int G, int cls) {
+  if (cls >= NCLS - 1) return 0;
+  if (cadmm_auxm(cls) && cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, 2) <= LDS_WAVE_BUDGET)
+    return 2;
+  if (cls >= ROWLDS_MIN_CLS && cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, 1) <= LDS_WAVE_BUDGET)
+    return 1;
+  return 0;
 }
 // dynamic LDS of a k_cadmm workgroup: the largest carve of the env classes that can occur (without a
 // forest every scenario is class 0, so the launch needs only that carve and more workgroups fit a CU)
 __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NCLS - 1) {
   size_t m = 0;
   for (int c = 0; c <= max_cls; ++c) {
-    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_rows_lds(n, G, c));
+    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_row_mode(n, G, c));
     m = b > m ? b : m;
   }
   return m;
@@ -206,7 +229,7 @@ struct CadmmLds {
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
 };
-__device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool lrows) {
+__device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int rmode) {
   CadmmLds L;
   L.fbar = smem;
   L.Rt = L.fbar + al2(G * 3 * n);
@@ -216,7 +239,7 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, bool
   L.wmx = L.sid + 64;
   L.rows = (double*)(L.wmx + 64);
   L.red = L.rows;
-  const int ra = lrows ? row_lds_doubles(cadmm_nr(cls)) : 0;
+  const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
   return L;
 }
@@ -514,8 +537,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   const int lsc = ls < G ? ls : 0;
   const int cnt = a.scount[CLS], first = a.scount[NCLS + CLS];
   if (cnt == 0) return;
-  const bool lrows = cadmm_rows_lds(n, G, CLS);  // wave-uniform
-  CadmmLds L = cadmm_carve(smem, n, G, CLS, lrows);
+  const int rmode = cadmm_row_mode(n, G, CLS);  // wave-uniform
+  CadmmLds L = cadmm_carve(smem, n, G, CLS, rmode);
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * RT_STRIDE * n;
   double* myred = L.red + lane * RDS;
@@ -527,6 +550,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   __syncthreads();
 
   // per-lane state of the slot's current scenario
+  DAT_PHASE_INIT(9);
   QPLane<1> P;
   int sc = -1;  // scenario of this lane's slot (-1: empty)
   const double* prm = nullptr;
@@ -539,6 +563,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   WaveCounters wc;
   for (;;) {
     // ---- refill empty slots from the queue
+    DAT_PHASE(11);
     if (lane < NT && i == 0 && L.sid[ls] == -1) {
       const int q = atomicAdd(a.qhead + CLS, 1);
       L.sid[ls] = q < cnt ? a.slist[first + q] : -2;  // -2: queue drained, slot retires
@@ -565,6 +590,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
     }
     if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
+    DAT_PHASE(12);
     if (fresh) {
       lane_cadmm_static(P, prm, i);
       if (ENV) {
@@ -593,8 +619,13 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
       double y[1][3], w[6];
       IPMOut o;
-      if constexpr (CLS >= ROWLDS_MIN_CLS && CLS < NCLS - 1) {
-        if (lrows)
+      DAT_PHASE(10);
+      constexpr unsigned AUXM = cadmm_auxm(CLS);
+      if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
+        if (AUXM != 0 && rmode == 2)
+          o = ipm_solve<MODE_CADMM, 1, NR, LdsRef<QPShared>, EnvLdsN<NE>, RtLds, RowLds, AUXM>(
+              shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL, RowLds{L.rows, lane});
+        else if (CLS >= ROWLDS_MIN_CLS && rmode == 1)
           o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                            IPM_TOL, RowLds{L.rows, lane});
         else
@@ -604,6 +635,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                          IPM_TOL);
       }
+      DAT_PHASE(9);
       wc.ipm += o.iters;
       wc.inband += o.inband;
       wc.loose += inband_loose(o);
@@ -623,6 +655,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         for (int c = 0; c < N3; ++c) myf[c] = prm[DAT_P_FEQ(n) + c];
       }  // otherwise hold the previous solution (control/rqp_cadmm.py:496-499)
     }
+    DAT_PHASE(13);
     wc.slot += wave_max(it_lane);
     ++wc.pass;
     if (active) atomicMax(&L.wmx[ls], it_lane);
@@ -1753,6 +1786,17 @@ int finish_hl(dat_handle* h) {
 }  // namespace
 
 extern "C" {
+
+#ifdef DAT_PHASE_PROF
+// development builds only (tools/phase_prof.py): the IPM phase cycle sums, reset after the read
+int dat_get_phase_cycles(unsigned long long* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dat::g_phase), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dat::g_phase), z, sizeof(z)));
+  return 0;
+}
+#endif
 
 void dat_default_config(dat_config* c) {
   memset(c, 0, sizeof(*c));

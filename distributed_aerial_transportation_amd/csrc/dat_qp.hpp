@@ -567,6 +567,31 @@ __host__ __device__ constexpr int ipm_aux_doubles(int NB, unsigned AUXM) {
 }
 __host__ __device__ constexpr int row_lds_doubles(int NR, int NX = 0) { return (3 * NR + NX) * 64; }  // (s, z) pairs, zw, aux
 
+// Phase profile (development builds only, -DDAT_PHASE_PROF): shader-clock cycles per phase of the
+// IPM iteration, summed over wavefronts by the first active lane (tools/phase_prof.py).
+#if defined(DAT_PHASE_PROF)
+__device__ unsigned long long g_phase[16];
+#endif
+#if defined(DAT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
+struct PhaseClock {
+  unsigned long long t0;
+  int cur;
+  __device__ PhaseClock(int c) : t0(clock64()), cur(c) {}
+  __device__ void to(int next) {
+    const unsigned long long t = clock64();
+    const unsigned long long act = __ballot(1);
+    if ((int)__lane_id() == __ffsll((long long)act) - 1) atomicAdd(&g_phase[cur], t - t0);
+    t0 = t;
+    cur = next;
+  }
+};
+#define DAT_PHASE_INIT(c) PhaseClock pclk_(c)
+#define DAT_PHASE(c) pclk_.to(c)
+#else
+#define DAT_PHASE_INIT(c)
+#define DAT_PHASE(c)
+#endif
+
 struct IPMOut {
   int status;
   int iters;
@@ -641,6 +666,22 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     const double* x = l < NWROW ? dw : dv;
     double a[3];
     ra3(l, a);
+    return a[0] * x[0] + a[1] * x[1] + a[2] * x[2];
+  };
+  // coefficients and constant of row l in one visit (base rows: two pair reads of the (a, b) record;
+  // env rows: two pair fields)
+  auto rowld = [&](int l, double* a, double& b) {
+    if (l < NBASE) {
+      double r4[4];
+      ldn<4>(sh.get().rows[l < NBASE ? l : 0], r4);
+      a[0] = r4[0]; a[1] = r4[1]; a[2] = r4[2];
+      b = r4[3];
+    } else {
+      er.ab(l >= NBASE ? l - NBASE : 0, a, b);
+    }
+  };
+  auto dot3x = [&](int l, const double* a, const double* v, const double* w) -> double {
+    const double* x = l < NWROW ? w : v;
     return a[0] * x[0] + a[1] * x[1] + a[2] * x[2];
   };
   // a_l . (dvl or dwl) + b_l
@@ -838,7 +879,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
   const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
 
+  DAT_PHASE_INIT(0);
   for (int it = 0;; ++it) {
+    DAT_PHASE(1);
     // ------------- residuals
     double dv[3], dw[3];
     double dres = 0.0, pres = 0.0, gap = 0.0;
@@ -927,6 +970,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         out.merit = merit;
 #pragma unroll
         for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
+        DAT_PHASE(8);
         return out;
       }
       // Only an in-band iterate (scaled residuals < 1e-7, gap < 1e-6) can be returned: a solve that
@@ -956,6 +1000,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     }
 
     // ------------- NT scaling of the cone blocks
+    DAT_PHASE(2);
     SocScale S1[NB], S2[NB];
     bool okc = true;
 #pragma unroll
@@ -1017,6 +1062,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       out.why = 4;
       break;
     }
+    DAT_PHASE(3);
     // M = Lm Lm' (Cholesky; M is SPD: C carries k_f, k_m > 0) and, for CADMM / CENT, the Cholesky
     // factor Ln of the SPD matrix N = I + Lm' T Lm, so that (I + M T)^-1 M = Lm N^-1 Lm' =: P.  N has
     // every eigenvalue >= 1 however large active rows make M, so the factorisation stays well
@@ -1240,13 +1286,14 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
-        double sl, zl;
+        double sl, zl, al3[3], bl;
         rst.sz(l, sl, zl);
+        rowld(l, al3, bl);
         const double is = frcp(sl);
-        const double rzl = sl - (rowval(l, dv, dw));
+        const double rzl = sl - (dot3x(l, al3, dv, dw) + bl);
         double cadd = 0.0;
         if (corr) {
-          const double a = rowdot(l, ddva, ddwa);
+          const double a = dot3x(l, al3, ddva, ddwa);
           cadd = act(l) * ((-rzl + a) * (ZW(l) - zl * is * a) - sigmu);
         }
         ZW(l) = (zl * rzl - (sl * zl + cadd)) * is;
@@ -1279,12 +1326,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0}, adz[6];
 #pragma unroll
           for (int l = 0; l < NR; ++l) {
-            double sl, zl;
+            double sl, zl, a[3];
             rst.sz(l, sl, zl);
-            const double dzl = ZW(l) - zl * frcp(sl) * rowdot(l, ddv, ddw);
-            double* g = l < NWROW ? gw : gv;
-            double a[3];
             ra3(l, a);
+            const double dzl = ZW(l) - zl * frcp(sl) * dot3x(l, a, ddv, ddw);
+            double* g = l < NWROW ? gw : gv;
             g[0] += dzl * a[0]; g[1] += dzl * a[1]; g[2] += dzl * a[2];
           }
           adj(gv, gw, adz);
@@ -1341,11 +1387,15 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     // row directions of the current Newton solution
     // (s_l, z_l) of the row: sl, zl (one pair read by the caller)
     auto row_dirs = [&](int l, const double* ddv, const double* ddw, double sl, double zl, double& ds, double& dz) {
-      const double a = rowdot(l, ddv, ddw);
-      ds = -(sl - (rowval(l, dv, dw))) + a;
+      double al3[3], bl;
+      rowld(l, al3, bl);
+      const double a = dot3x(l, al3, ddv, ddw);
+      ds = -(sl - (dot3x(l, al3, dv, dw) + bl)) + a;
       dz = ZW(l) - zl * frcp(sl) * a;
     };
-    auto step_len = [&]() {
+    // step_len / gap_at / the update take the row-space image (ddv, ddw) = lin(du) of the current
+    // direction, computed once per direction by the caller
+    auto step_len = [&](const double* ddv, const double* ddw) {
       double a = 1e300;
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -1363,8 +1413,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         a = fmin(a, soc_step(l4, dss + 5));
         a = fmin(a, soc_step(l4, dzs_k[k] + 5));
       }
-      double ddv[3], ddw[3];
-      lin(du, ddv, ddw);
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
@@ -1376,7 +1424,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
       return a;
     };
-    auto gap_at = [&](double al) {
+    auto gap_at = [&](double al, const double* ddv, const double* ddw) {
       double g = 0.0;
 #pragma unroll
       for (int k = 0; k < NB; ++k)
@@ -1386,8 +1434,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           const double lj = LAM(k, j);
           g += (lj + al * dss) * (lj + al * dzs_k[k][j]);
         }
-      double ddv[3], ddw[3];
-      lin(du, ddv, ddw);
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
@@ -1400,6 +1446,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     };
 
     // predictor
+    DAT_PHASE(4);
     {
       double rsk[NB][9];
 #pragma unroll
@@ -1415,8 +1462,11 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       newton(rsk, false, nullptr, nullptr, 0.0);
     }
     {
-      const double aaff = fmin(1.0, step_len());
-      const double gaff = gap_at(aaff);
+      DAT_PHASE(5);
+      double ddva[3], ddwa[3];  // lin(du) of the affine direction: its step, gap and the corrector's term
+      lin(du, ddva, ddwa);
+      const double aaff = fmin(1.0, step_len(ddva, ddwa));
+      const double gaff = gap_at(aaff, ddva, ddwa);
       double sig = gaff / gap;
       sig = fmax(0.0, fmin(1.0, sig * sig * sig));
       const double sigmu = sig * gap * ideg;
@@ -1441,16 +1491,18 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         rsk[k][1] -= sigmu;
         rsk[k][5] -= sigmu;
       }
-      double ddva[3], ddwa[3];
-      lin(du, ddva, ddwa);
+      DAT_PHASE(6);
       newton(rsk, true, ddva, ddwa, sigmu);
     }
-    double alpha = fmin(1.0, ETA * step_len());
+    DAT_PHASE(7);
+    double ddv[3], ddw[3];  // lin(du) of the corrector direction
+    lin(du, ddv, ddw);
+    double alpha = fmin(1.0, ETA * step_len(ddv, ddw));
     // safeguard: Mehrotra's corrector can increase the gap of a feasible iterate (it then cycles);
     // backtrack until the complementarity gap decreases
     const bool feasible = pres < 1e-8 * NH() && dres < 1e-8 * NQ();
     for (int bt = 0; feasible && bt < 8; ++bt) {
-      if (gap_at(alpha) <= gap * (1.0 - 0.01 * alpha)) break;
+      if (gap_at(alpha, ddv, ddw) <= gap * (1.0 - 0.01 * alpha)) break;
       alpha *= 0.5;
     }
     // update.  ds from the primal equation (keeps G y + s = h exact), dz = W^-1 dzs.
@@ -1471,8 +1523,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
     for (int r = 0; r < 6; ++r) w[r] += alpha * dwv[r];
     {
-      double ddv[3], ddw[3];
-      lin(du, ddv, ddw);
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
@@ -1483,6 +1533,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
     }
   }
+  DAT_PHASE(8);
   // not converged to tol: return the best iterate seen; "optimal" if its scaled primal / dual
   // residuals are within north_star's 1e-7 and its complementarity gap within 1e-6 (strongly graded
   // problems -- the rigid payload's Jl^-1 ~ 50 -- can stall at a 1e-7 gap while the structured Newton

@@ -20,6 +20,8 @@ for k in range(int(round(T / 1e-2))):
     F.append(r.f_des[0].copy()), I.append(r.iters[0]), MD.append(r.min_env_dist[0]), QS.append(r.qp_status[0].copy())
     if k % 1000 == 0:
         print(k, flush=True)
+        np.savez(f"gpurun_out/long_{ct.split('-')[0][:4]}.npz", f_des=np.array(F), iters=np.array(I), min_dist=np.array(MD),
+                 states=np.array(X), qp_status=np.array(QS))
     eng.rollout(10)
 tag = ct.split("-")[0][:4]
 np.savez(f"gpurun_out/long_{tag}.npz", f_des=np.array(F), iters=np.array(I), min_dist=np.array(MD), states=np.array(X), qp_status=np.array(QS))
