@@ -1,0 +1,38 @@
+"""Hard closed-loop stretches (tests/golden/make_hard_stretch.py): from a recorded state the
+controller itself runs into trouble -- DD's dual ascent climbs 12 -> 59 iterations and stalls at
+max_iter for seven HL steps before recovering (control/rqp_dd.py:695-752); C-ADMM next to a tree stalls
+at max_iter from the 12th step on (control/rqp_cadmm.py:631-675) -- both inside the reference loop of
+example/rqp_example.py:120-131.  The GPU loop (cold warm state, the production kernels) must follow the
+oracle through it: iteration counts exact at every step, f_des within 1e-5 up to the first stalled
+step and within 1e-3 through the stall (max_iter iterations of dual ascent / consensus amplify
+solver-tolerance differences: the oracle's own f_des moves by ~1e-4 there when its QP tolerance
+changes).  These are the states where the long-horizon runs (test_gpu_long.py) leave the reference's
+trajectory for good: the failure is the controller's, not the solver's."""
+
+import numpy as np
+import pytest
+
+from tests._golden import load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("ct,name", [("dual-decomposition", "ref_dd_hard.npz"), ("consensus-admm", "ref_cadmm_hard.npz")])
+def test_gpu_hard_stretch_matches_oracle(ct, name):
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+
+    d = load(name)
+    n, K = 3, d["f_des"].shape[0]
+    eng = BatchedController(ct, n, 1, scenarios.params_block(n))
+    eng.set_forests([Forest.seeded(0)])
+    eng.set_state(d["x0"][None], np.zeros(1, dtype=np.int32))
+    its = d["iters"].astype(int)
+    stall = int(np.argmax(its > 100))
+    assert stall > 0 and its.max() == 101
+    for k in range(K):
+        r = eng.control(None, None)
+        assert r.iters[0] == its[k], (k, r.iters[0], its[k])
+        ref = d["f_des"][k]
+        rel = np.max(np.abs(r.f_des[0] - ref)) / max(1.0, np.max(np.abs(ref)))
+        assert rel < (1e-5 if k < stall else 1e-3), (k, rel)
+        eng.rollout(10)
