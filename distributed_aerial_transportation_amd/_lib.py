@@ -17,8 +17,11 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libdat.so")
 SRC = os.path.join(PKG, "csrc", "dat.hip")
-DEPS = [SRC, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_qp.hpp"),
-        os.path.join(PKG, "csrc", "dat_layout.h"),
+SRC_CENT = os.path.join(PKG, "csrc", "dat_cent.hip")  # k_cent<n>: its own translation unit, compiled in parallel
+OBJ_DIR = os.path.join(PKG, "build")
+HIPFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
+DEPS = [SRC, SRC_CENT, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_qp.hpp"),
+        os.path.join(PKG, "csrc", "dat_kargs.hpp"), os.path.join(PKG, "csrc", "dat_layout.h"),
         os.path.join(REPO, "include", "dat.h")]
 
 MODE_CENTRALIZED, MODE_CADMM, MODE_DD = 0, 1, 2
@@ -69,14 +72,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
         with open(STAMP) as f:
             have = f.read().strip()
     if force or have != want:
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", SRC, "-o", LIB_PATH]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        os.makedirs(OBJ_DIR, exist_ok=True)
+        objs = [os.path.join(OBJ_DIR, os.path.basename(src) + ".o") for src in (SRC, SRC_CENT)]
+        cmds = [["hipcc"] + HIPFLAGS + ["-c", src, "-o", o] for src, o in zip((SRC, SRC_CENT), objs)]
+        procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for c in cmds]
+        for c, pr in zip(cmds, procs):
+            _, err = pr.communicate()
+            if pr.returncode != 0:
+                raise DatError("hipcc failed: " + " ".join(c) + "\n" + err[-4000:])
+        link = ["hipcc"] + HIPFLAGS + ["-shared"] + objs + ["-o", LIB_PATH]
+        r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
-            raise DatError("hipcc failed:\n" + r.stderr[-4000:])
+            raise DatError("hipcc link failed:\n" + r.stderr[-4000:])
         with open(STAMP, "w") as f:
             f.write(want + "\n")
         if verbose:
-            print(" ".join(cmd))
+            for c in cmds + [link]:
+                print(" ".join(c))
     return LIB_PATH
 
 

@@ -9,7 +9,7 @@
 //              (control/rqp_dd.py:513-555, 634-657).
 //   k_dd       DD control step: prices, agent QPs, consensus error, dual ascent through H^-1
 //              (control/rqp_dd.py:659-752).
-//   k_cent     centralized QP, one lane per scenario (control/rqp_centralized.py:436-448).
+//   k_cent     centralized QP, one lane per scenario (control/rqp_centralized.py:436-448): dat_cent.hip.
 //   k_rollout_agents  low-level SO(3) law + dynamics + Lie integration, one lane per agent.
 //   k_desired  forest desired-acceleration law (example/rqp_example.py:33-59).
 #include <hip/hip_runtime.h>
@@ -23,7 +23,7 @@
 #include <algorithm>
 
 #include "../../include/dat.h"
-#include "dat_qp.hpp"
+#include "dat_kargs.hpp"
 
 using namespace dat;
 
@@ -41,95 +41,6 @@ int fail(const std::string& m) {
     hipError_t e_ = (x);                                                          \
     if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
-
-constexpr int NMAX = 16;        // largest team the kernels are compiled for
-constexpr int NMAX_DD = 8;      // DD master matrix is (6n)^2 in LDS
-constexpr int IPM_MAX_ITER = 50;
-constexpr double IPM_TOL = 1e-10;
-// C-ADMM env classes (cadmm_block<C>): 0 no env row, then the largest per-agent env-row count of the
-// scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
-constexpr int NCLS = 4;
-__host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 5 : DAT_NENV; }
-// k_bucket sort key: class x bin of the scenario's previous ADMM iteration count (1, 2, 3, 4-5,
-// 6-9, 10-17, 18-33, >= 34), so that scenarios sharing a wavefront tend to need the same number of
-// ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
-// tail of the whole launch)
-constexpr int NAB = 8;   // ADMM / DD iteration bins
-constexpr int NPB = 4;   // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
-constexpr int NIB = NAB * NPB;
-__host__ __device__ inline int iter_bin(int it) {
-  if (it <= 3) return it < 1 ? 0 : it - 1;
-  const int lg = 31 - __builtin_clz((unsigned)(it - 2));  // floor(log2(it - 2)) >= 1
-  return 2 + lg < NAB - 1 ? 2 + lg : NAB - 1;
-}
-// IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8
-__host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
-constexpr int NKEY = NCLS * NIB;
-constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
-// QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
-// scaled residual / gap exceeds Clarabel's own tolerance (INBAND_CLARABEL)
-constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
-constexpr int DAT_NCOUNTERS = CNT_INBAND + 2;
-constexpr double INBAND_CLARABEL = 1e-8;
-__device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
-
-struct KArgs {
-  int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)
-  const double* params;
-  double* state;
-  int* counter;
-  const double* acc;
-  double* fdes;
-  const double* trees;
-  const int* tree_off;
-  const int* scen_forest;
-  int nforest;
-  const double* mountain;
-  int max_iter;
-  double res_tol;
-  int use_total_res;
-  double rho0, tau, rho_max;
-  int record_err;
-  double *cf, *cfbar, *clam;                 // C-ADMM warm state
-  double *dlamF, *dlamM, *dprev, *dHinv;      // DD state
-  double* pf;                                 // centralized previous solution
-  double* best;                               // lane-private best-iterate records of the IPM
-  int* iters;
-  int* qstatus;
-  double* mind;
-  unsigned char* col;
-  double* err;
-  unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
-                                 // (C-ADMM: [CNT_STRIDE k + .] per env class k, cadmm_block<k>)
-  int G;                         // C-ADMM: scenario slots per k_cadmm wavefront (cadmm_slots)
-  int* need;                     // C-ADMM: per-scenario sort key of the step (k_env_class)
-  int* ipmx;                     // C-ADMM: IPM iterations of the scenario's slowest agent QP, previous step
-  int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
-  int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
-  int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
-  double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
-                                 //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
-  unsigned* emask;               // C-ADMM: [B n] env row mask of the step
-  int ll_kind;                   // low-level SO(3) law: LL_PD or LL_SM (dat_set_low_level)
-};
-
-// wave-uniform maximum (every lane of the wavefront must execute it)
-__device__ inline int wave_max(int v) {
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-  return v;
-}
-
-__device__ inline const double* prm_of(const KArgs& a, int sc) { return a.params + (a.ppp ? (size_t)sc * a.P : 0); }
-
-__device__ inline void forest_of(const KArgs& a, int sc, const double** trees, int* nt) {
-  *trees = nullptr;
-  *nt = 0;
-  if (a.nforest <= 0) return;
-  int f = a.scen_forest ? a.scen_forest[sc] : 0;
-  if (f < 0 || f >= a.nforest) return;
-  *trees = a.trees + 3 * (size_t)a.tree_off[f];
-  *nt = a.tree_off[f + 1] - a.tree_off[f];
-}
 
 // ------------------------------------------------------------------------------------------------
 // C-ADMM
@@ -836,13 +747,120 @@ __device__ void dd_strong_convexity(const double* prm, int n, const double* st, 
   }
 }
 
+// k_dd_setup keeps the columns of [H | I] in registers for n <= DD_REG_NMAX (dd_setup_h_regs), in LDS
+// beyond
+constexpr int DD_REG_NMAX = 8;
 // doubles of the [H | I] area of k_dd_setup; it first holds the per-agent [Q_i | I] (162 n), their
-// pivot columns (9 n) and pivot rows (n ints)
+// pivot columns (9 n) and pivot rows (n ints).  Register path: the Q_i area and two N-double pivot
+// column buffers only.
 __host__ __device__ inline int dd_setup_hs(int n) {
   const int N = 6 * n;
+  if (n <= DD_REG_NMAX) return 171 * n + 1 + 2 * N;  // k_dd_setup<n>
   return 2 * N * N > 171 * n + 1 ? 2 * N * N : 171 * n + 1;
 }
 
+// H = A blkdiag(Q_j^-1) A' (control/rqp_dd.py:642-655) and H^-1 by Gauss-Jordan on [H | I], n = NB,
+// with the columns of [H | I] in registers: lane c owns column c and, when 2N > 64, column c + 64 (an
+// identity column: N <= 48).  Same per-element arithmetic and order as the LDS path, so the result is
+// bitwise equal: H_rc summed over blocks j, then over the support p of row r's block in increasing
+// order, of A_rp (Q_j A_c)_p with (Q_j A_c)_p summed over q in increasing order; Gauss-Jordan without
+// pivoting (H is SPD), per element hk = h_kc / piv, h_rc -= f_r hk.  The column is kept rotated so
+// that step k's pivot row is element 0 (no runtime register index): the owner of column k publishes it
+// in LDS (double buffered), every lane updates its columns and rotates them by one.
+template <int NB>
+__device__ void dd_setup_h_regs(const KArgs& a, int sc, const double* Qi, const double* Rts, double* fac) {
+  constexpr int N = 6 * NB;
+  constexpr bool TWO = 2 * N > 64;
+  const int lane = threadIdx.x;
+  double h[N], g[TWO ? N : 1];
+  // ---- assembly of column lane (H columns for lane < N, identity columns e_{lane - N} beyond)
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    h[r] = (lane >= N && r == lane - N) ? 1.0 : 0.0;
+    if (TWO) g[r] = (r == lane + 64 - N) ? 1.0 : 0.0;
+  }
+  if (lane < N) {
+    const int ag = lane / 6, comp = lane - 6 * ag;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const double* Q = Qi + 81 * j;
+      // w = Q_j a_{c,j}: a_{c,j} = e_{3+comp} (j == ag), -e_comp (comp < 3), -Rt_j[comp-3, :] on f_j
+      double w[9];
+      if (j == ag) {
+#pragma unroll
+        for (int p = 0; p < 9; ++p) { double t = 0.0; t += Q[9 * p + 3 + comp] * 1.0; w[p] = t; }
+      } else if (comp < 3) {
+#pragma unroll
+        for (int p = 0; p < 9; ++p) { double t = 0.0; t += Q[9 * p + comp] * -1.0; w[p] = t; }
+      } else {
+        const double* rt = Rts + 9 * j + 3 * (comp - 3);
+        const double v0 = -rt[0], v1 = -rt[1], v2 = -rt[2];
+#pragma unroll
+        for (int p = 0; p < 9; ++p) {
+          double t = 0.0;
+          t += Q[9 * p] * v0;
+          t += Q[9 * p + 1] * v1;
+          t += Q[9 * p + 2] * v2;
+          w[p] = t;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < N; ++r) {
+        const int agr = r / 6, cr = r % 6;
+        if (j == agr) {
+          h[r] += 1.0 * w[3 + cr];
+        } else if (cr < 3) {
+          h[r] += -1.0 * w[cr];
+        } else {
+          const double* rt = Rts + 9 * j + 3 * (cr - 3);
+          h[r] += -rt[0] * w[0];
+          h[r] += -rt[1] * w[1];
+          h[r] += -rt[2] * w[2];
+        }
+      }
+    }
+  }
+  // ---- Gauss-Jordan, columns rotated (h[i] = [H | I]_{(k + i) mod N, c} at step k)
+  for (int k = 0; k < N; ++k) {
+    double* f = fac + (k & 1) * N;
+    if (lane == k) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) f[i] = h[i];
+    }
+    __syncthreads();
+    const double piv = f[0];
+    {
+      const double hk = h[0] / piv;
+#pragma unroll
+      for (int i = 1; i < N; ++i) h[i] -= f[i] * hk;
+#pragma unroll
+      for (int i = 0; i < N - 1; ++i) h[i] = h[i + 1];
+      h[N - 1] = hk;
+    }
+    if (TWO) {
+      const double hk = g[0] / piv;
+#pragma unroll
+      for (int i = 1; i < N; ++i) g[i] -= f[i] * hk;
+#pragma unroll
+      for (int i = 0; i < N - 1; ++i) g[i] = g[i + 1];
+      g[N - 1] = hk;
+    }
+  }
+  // ---- H^-1 = the right half: column N + c' of [H | I] is column c' of H^-1 (row-major output)
+  double* out = a.dHinv + (size_t)sc * N * N;
+  if (lane >= N && lane < 2 * N) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) out[(size_t)r * N + (lane - N)] = h[r];
+  }
+  if (TWO && lane + 64 < 2 * N) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) out[(size_t)r * N + (lane + 64 - N)] = g[r];
+  }
+}
+
+// NB = n (<= DD_REG_NMAX: H columns in registers, one instantiation per team size so each has its own
+// register footprint) or 0 (any n: H in LDS)
+template <int NB>
 __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N = 6 * n;
@@ -906,6 +924,10 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
     Qi[e] = 0.5 * (A[18 * r + 9 + c] + A[18 * c + 9 + r]);
   }
   __syncthreads();
+  if constexpr (NB > 0) {
+    dd_setup_h_regs<NB>(a, sc, Qi, Rts, H + 171 * n + 1);  // pivot columns past the Q_i elimination area
+    return;
+  }
   // H = A blkdiag(Q_j^-1) A'  (control/rqp_dd.py:642-655); row r of A restricted to block j:
   //   j == agent(r): unit vector e_{3 + comp};  j != agent(r): -e_comp (comp < 3) or -Rt_j[comp-3, :] on f_j
   // every index below is compile-time after unrolling, so v stays in registers (no scratch)
@@ -968,7 +990,15 @@ constexpr int DD_ES = 7, DD_RS = 5;
 // k_dd per-wavefront area: with a forest the env rows' LDS image; without one nothing (n = 6:
 // 27.0 KB, four wavefronts per CU -- the unused 20 KB image used to hold k_dd at three, C3 A/B
 // 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers (RowLds measured 26.2 ms).
-__host__ __device__ constexpr int dd_area_doubles(bool env) { return env ? ENV_LDS_DOUBLES : 0; }
+// Without a forest the 3 base rows' IPM state (s, z pairs and zw) lives in this area instead (RowLds):
+// with the pair layout it removes the DD agent QP's scratch spills (probe: 52 scratch ops -> 0 per
+// IPM pass for 60 more LDS reads).
+#ifndef DAT_DD_ROWLDS
+#define DAT_DD_ROWLDS 1
+#endif
+__host__ __device__ constexpr int dd_area_doubles(bool env) {
+  return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE) : 0);
+}
 // k_dd_key: drain-order key of every scenario (previous step's DD iteration count, longest first),
 // sorted by k_bucket into one queue (class 0).
 __global__ void k_dd_key(KArgs a) {
@@ -1088,6 +1118,9 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       if constexpr (ENV)
         o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                        IPM_TOL);
+      else if constexpr (DAT_DD_ROWLDS)
+        o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+                                         IPM_TOL, RowLds{envs, lane});
       else
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                          IPM_TOL);
@@ -1200,74 +1233,6 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     lo += __shfl_xor(lo, off);
   }
   if (lane == 0) {
-    atomicAdd(a.counters, q);
-    atomicAdd(a.counters + 1, ip);
-    atomicAdd(a.counters + 2, rw);
-    if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
-    if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// centralized: one lane per scenario
-// ------------------------------------------------------------------------------------------------
-template <int NB>
-__global__ __launch_bounds__(64) void k_cent(KArgs a) {
-  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = sc < a.B;
-  const int n = NB;
-  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0;
-  const double* prm = valid ? prm_of(a, sc) : a.params;
-  QPShared S;
-  QPLane<NB> P;
-  double Rt[NB][9];
-  EnvRows E;
-  EnvOut env;
-  env.collision = 0;
-  env.min_env_dist = 0.0;
-  int nr = NBASE;
-  if (valid) {
-    const double* st = a.state + (size_t)sc * a.S;
-    build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
-    lane_cent<NB>(P, prm, n, st, Rt);
-    const double* trees;
-    int nt;
-    unsigned emask;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &emask, lhs, rhs);
-    set_env_rows(P, E, S, emask, lhs, rhs);
-    nr = rows_needed(P.emask);
-  }
-  nr = wave_max(nr);
-  if (valid) {
-    double y[NB][3], w[6];
-    IPMOut o = ipm_solve_rows<MODE_CENT, NB>(nr, PlainRef<QPShared>{&S}, EnvPlain{&E}, RtPtr{&Rt[0][0]}, P,
-                                             prm + DAT_P_FEQ(n), y, w, a.best + (size_t)sc * best_size(NB),
-                                             IPM_MAX_ITER, IPM_TOL);
-    q = 1;
-    ip = o.iters;
-    ib = o.inband;
-    lo = inband_loose(o);
-    rw = (unsigned long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
-    double* pf = a.pf + (size_t)sc * 3 * n;
-    if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
-      for (int k = 0; k < NB; ++k)
-        for (int c = 0; c < 3; ++c) pf[3 * k + c] = y[k][c];
-    for (int c = 0; c < 3 * n; ++c) a.fdes[(size_t)sc * 3 * n + c] = pf[c];
-    for (int k = 0; k < n; ++k) a.qstatus[(size_t)sc * n + k] = o.status;
-    a.iters[sc] = -1;
-    a.col[sc] = (unsigned char)env.collision;
-    a.mind[sc] = env.min_env_dist;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    q += __shfl_xor(q, off);
-    ip += __shfl_xor(ip, off);
-    rw += __shfl_xor(rw, off);
-    ib += __shfl_xor(ib, off);
-    lo += __shfl_xor(lo, off);
-  }
-  if (threadIdx.x == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
     atomicAdd(a.counters + 2, rw);
@@ -1747,7 +1712,18 @@ int launch_hl(dat_handle* h) {
     hipLaunchKernelGGL(k_cadmm, dim3(std::min(cblocks, h->persistent_blocks)), dim3(64),
                        cadmm_lds_bytes(n, Gc, h->nforest > 0 ? NCLS - 1 : 0), h->stream, a);
   } else if (h->cfg.mode == DAT_MODE_DD) {
-    hipLaunchKernelGGL(k_dd_setup, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a);
+    if (n > DD_REG_NMAX)  // [H | I] in LDS: beyond the default 64 KB dynamic LDS from n = 11 on
+      HIPCHK(hipFuncSetAttribute((const void*)k_dd_setup<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)dd_setup_lds(n)));
+    switch (n <= DD_REG_NMAX ? n : 0) {
+      case 3: hipLaunchKernelGGL(k_dd_setup<3>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      case 4: hipLaunchKernelGGL(k_dd_setup<4>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      case 5: hipLaunchKernelGGL(k_dd_setup<5>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      case 6: hipLaunchKernelGGL(k_dd_setup<6>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      case 7: hipLaunchKernelGGL(k_dd_setup<7>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      case 8: hipLaunchKernelGGL(k_dd_setup<8>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+      default: hipLaunchKernelGGL(k_dd_setup<0>, dim3(B), dim3(64), dd_setup_lds(n), h->stream, a); break;
+    }
     hipLaunchKernelGGL(k_dd_key, dim3((B + 63) / 64), dim3(64), 0, h->stream, a);
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
@@ -1759,10 +1735,7 @@ int launch_hl(dat_handle* h) {
       hipLaunchKernelGGL(k_dd<false>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n, h->nforest > 0), h->stream, a);
   } else {
     int blocks = (B + 63) / 64;
-    if (n == 3)
-      hipLaunchKernelGGL(k_cent<3>, dim3(blocks), dim3(64), 0, h->stream, a);
-    else
-      hipLaunchKernelGGL(k_cent<6>, dim3(blocks), dim3(64), 0, h->stream, a);
+    HIPCHK(launch_cent(n, blocks, h->stream, a));
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(h->e1, h->stream));
@@ -1828,8 +1801,8 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   *out = nullptr;
   const dat_config& c = *cfg;
   if (c.n < 3 || c.n > NMAX) return fail("dat_create: n must be in [3, 16]");
-  if (c.mode == DAT_MODE_DD && c.n > NMAX_DD) return fail("dat_create: DD supports n <= 8");
-  if (c.mode == DAT_MODE_CENTRALIZED && c.n != 3 && c.n != 6) return fail("dat_create: centralized supports n in {3, 6}");
+  if (c.mode == DAT_MODE_DD && c.n > NMAX_DD) return fail("dat_create: DD supports n <= 16");
+  if (c.mode == DAT_MODE_CENTRALIZED && c.n > NMAX_CENT) return fail("dat_create: centralized supports n <= 6");
   if (c.mode < 0 || c.mode > 2) return fail("dat_create: bad mode");
   if (c.batch < 1) return fail("dat_create: batch must be >= 1");
   if (c.max_iter < 0) return fail("dat_create: max_iter must be >= 0");

@@ -1,0 +1,105 @@
+// dat_kargs.hpp -- kernel arguments and launch-wide constants shared by the translation units of
+// libdat.so (dat.hip: C-ADMM, DD, rollout, C-ABI; dat_cent.hip: the centralized kernel).
+#pragma once
+
+#include "dat_qp.hpp"
+
+namespace dat {
+
+constexpr int NMAX = 16;        // largest team the kernels are compiled for
+constexpr int NMAX_DD = 16;     // DD: k_dd_setup<0> keeps [H | I] (2 (6n)^2 doubles) in LDS: 144 KB at n = 16
+constexpr int IPM_MAX_ITER = 50;
+constexpr double IPM_TOL = 1e-10;
+// C-ADMM env classes (cadmm_block<C>): 0 no env row, then the largest per-agent env-row count of the
+// scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
+constexpr int NCLS = 4;
+__host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c == 1 ? 2 : c == 2 ? 5 : DAT_NENV; }
+// k_bucket sort key: class x bin of the scenario's previous ADMM iteration count (1, 2, 3, 4-5,
+// 6-9, 10-17, 18-33, >= 34), so that scenarios sharing a wavefront tend to need the same number of
+// ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
+// tail of the whole launch)
+constexpr int NAB = 8;   // ADMM / DD iteration bins
+constexpr int NPB = 4;   // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
+constexpr int NIB = NAB * NPB;
+__host__ __device__ inline int iter_bin(int it) {
+  if (it <= 3) return it < 1 ? 0 : it - 1;
+  const int lg = 31 - __builtin_clz((unsigned)(it - 2));  // floor(log2(it - 2)) >= 1
+  return 2 + lg < NAB - 1 ? 2 + lg : NAB - 1;
+}
+// IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8
+__host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
+constexpr int NKEY = NCLS * NIB;
+constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
+// QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
+// scaled residual / gap exceeds Clarabel's own tolerance (INBAND_CLARABEL)
+constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
+constexpr int DAT_NCOUNTERS = CNT_INBAND + 2;
+constexpr double INBAND_CLARABEL = 1e-8;
+__device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
+
+struct KArgs {
+  int B, n, P, S, ppp;  // ppp: params per scenario (1) or broadcast (0)
+  const double* params;
+  double* state;
+  int* counter;
+  const double* acc;
+  double* fdes;
+  const double* trees;
+  const int* tree_off;
+  const int* scen_forest;
+  int nforest;
+  const double* mountain;
+  int max_iter;
+  double res_tol;
+  int use_total_res;
+  double rho0, tau, rho_max;
+  int record_err;
+  double *cf, *cfbar, *clam;                 // C-ADMM warm state
+  double *dlamF, *dlamM, *dprev, *dHinv;      // DD state
+  double* pf;                                 // centralized previous solution
+  double* best;                               // lane-private best-iterate records of the IPM
+  int* iters;
+  int* qstatus;
+  double* mind;
+  unsigned char* col;
+  double* err;
+  unsigned long long* counters;  // [0] agent-QP solves, [1] IPM iterations, [2] IPM iterations x active rows
+                                 // (C-ADMM: [CNT_STRIDE k + .] per env class k, cadmm_block<k>)
+  int G;                         // C-ADMM: scenario slots per k_cadmm wavefront (cadmm_slots)
+  int* need;                     // C-ADMM: per-scenario sort key of the step (k_env_class)
+  int* ipmx;                     // C-ADMM: IPM iterations of the scenario's slowest agent QP, previous step
+  int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
+  int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
+  int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
+  double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
+                                 //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
+  unsigned* emask;               // C-ADMM: [B n] env row mask of the step
+  int ll_kind;                   // low-level SO(3) law: LL_PD or LL_SM (dat_set_low_level)
+};
+
+// wave-uniform maximum (every lane of the wavefront must execute it)
+__device__ inline int wave_max(int v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
+__device__ inline const double* prm_of(const KArgs& a, int sc) { return a.params + (a.ppp ? (size_t)sc * a.P : 0); }
+
+__device__ inline void forest_of(const KArgs& a, int sc, const double** trees, int* nt) {
+  *trees = nullptr;
+  *nt = 0;
+  if (a.nforest <= 0) return;
+  int f = a.scen_forest ? a.scen_forest[sc] : 0;
+  if (f < 0 || f >= a.nforest) return;
+  *trees = a.trees + 3 * (size_t)a.tree_off[f];
+  *nt = a.tree_off[f + 1] - a.tree_off[f];
+}
+
+// centralized control step of every scenario (dat_cent.hip): k_cent<n> for 3 <= n <= NMAX_CENT.  One
+// lane holds a whole team's QP (3n forces, 3n cones): scratch grows ~1.2 KB/lane per agent (7.2 KB at
+// n = 6), and the n = 8 instance did not complete a 4-scenario step on MI355X within 3 minutes
+// (round 3), so larger teams use the distributed controllers (C-ADMM, DD: n <= 16).
+constexpr int NMAX_CENT = 6;
+hipError_t launch_cent(int n, int blocks, hipStream_t stream, const KArgs& a);
+
+}  // namespace dat

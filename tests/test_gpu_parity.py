@@ -24,6 +24,12 @@ REL = 1e-5
 # absolute at err ~ 1e-2), 1e-12 vs 1e-11 by 1.6e-5, while an explicit H^-1 instead of cho_solve
 # moves it by 2e-11.  The comparison is therefore rtol 1e-4 OR 2e-6 N absolute (1e-7 of m_T g).
 ERR_RTOL, ERR_ATOL = 1e-4, 2e-6
+# DD err_seq by team size where the oracle's own sensitivity is larger (tools/dd_sensitivity.py n: IPM
+# tolerance 1e-11 -> 1e-10 moves the oracle's err_seq by 1.05e-2 relative at n = 4, 7.7e-4 at n = 11
+# and 5.7e-3 at n = 16 -- those teams' agent QPs are strongly convex only through the 1e-6
+# regularisation in some directions, so the solution moves ~tol / 1e-6 -- against 4.3e-5 at n = 3,
+# 9.6e-5 at n = 6 and 2.7e-5 at n = 8): 3x the measured change.
+DD_ERR_RTOL = {4: 3e-2, 11: 2.5e-3, 16: 1.8e-2}
 
 
 def _eng(mode, n, B, **kw):
@@ -133,10 +139,11 @@ def _ambiguous(seq, tol=1e-2):
     return any(abs(e - tol) < 1e-7 * tol for e in seq)
 
 
-@pytest.mark.parametrize("n", [3, 6])
+@pytest.mark.parametrize("n", [3, 4, 6, 8, 11, 16])
 def test_gpu_dd_step_matches_oracle(n):
     """DD control step (control/rqp_dd.py:695-752) incl. the warm multipliers of a second step:
-    iteration counts exact, f_des within 1e-5, residual sequences within 1e-4 relative."""
+    iteration counts exact, f_des within 1e-5, residual sequences within 1e-4 relative.  n <= 8 runs
+    k_dd_setup<n> (H columns in registers), n = 11 and 16 the LDS path (k_dd_setup<0>, > 64 KB LDS)."""
     from distributed_aerial_transportation_amd import scenarios
 
     B = 6
@@ -157,8 +164,9 @@ def test_gpu_dd_step_matches_oracle(n):
             continue
         assert r1.iters[b] == st1.iter and r2.iters[b] == st2.iter, (b, r1.iters[b], st1.iter, r2.iters[b], st2.iter)
         assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL, (_rel(r1.f_des[b], f1), _rel(r2.f_des[b], f2))
-        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
-        np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=ERR_RTOL, atol=ERR_ATOL)
+        rtol = DD_ERR_RTOL.get(n, ERR_RTOL)
+        np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=rtol, atol=ERR_ATOL)
+        np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=rtol, atol=ERR_ATOL)
         assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
     assert skipped <= 1
     assert eng.work()["inband_beyond_clarabel_tol"] == 0
@@ -220,6 +228,29 @@ def test_gpu_dd_golden():
         assert _rel(r.f_des[0], d["tol_f"][k]) < REL
         it = int(d["tol_iters"][k])
         np.testing.assert_allclose(r.err_seq[0, : it - 1], d["tol_err"][k][: it - 1], rtol=ERR_RTOL, atol=ERR_ATOL)
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 6])
+def test_gpu_centralized_step_matches_oracle(n):
+    """Centralized control step (control/rqp_centralized.py:27-455, generic in n) for every team
+    size the kernel is instantiated for (k_cent<n>, dat_cent.hip): two steps (the held previous
+    solution persists), f_des within 1e-5 of the oracle's dense IPM, statuses OPTIMAL."""
+    from distributed_aerial_transportation_amd import scenarios
+
+    B = 4
+    rng = np.random.default_rng(40 + n)
+    states = scenarios.perturbed_states(n, B, rng)
+    acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
+    eng = _eng("centralized", n, B)
+    r1 = eng.control(states, acc)
+    r2 = eng.control(states, acc[::-1].copy())
+    for b in range(B):
+        ctl = oc.Centralized(osc.params(n), osc.col_radius(n))
+        s = _ostate(states[b], n)
+        f1, _ = ctl.control(s, (acc[b, :3], acc[b, 3:]))
+        f2, _ = ctl.control(s, (acc[B - 1 - b, :3], acc[B - 1 - b, 3:]))
+        assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL, (b, _rel(r1.f_des[b], f1), _rel(r2.f_des[b], f2))
+        assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
 
 
 def test_gpu_centralized_golden():

@@ -9,7 +9,7 @@ Measured (round 2): tol 1e-10 -> 9.6e-5 max relative change, 1e-9 -> 3.4e-3, 1e-
 explicit inverse -> 2.0e-11.  The DD err_seq drift between the GPU and the oracle is therefore the
 QP solve tolerance amplified by the consensus-error cancellation, not the H solve.
 
-    python tools/dd_sensitivity.py
+    python tools/dd_sensitivity.py [n]
 """
 
 import os
@@ -29,7 +29,7 @@ from distributed_aerial_transportation_amd.system import RQPState  # noqa: E402
 
 
 def main():
-    n, B = 6, 6
+    n, B = int(sys.argv[1]) if len(sys.argv) > 1 else 6, 6
     rng = np.random.default_rng(10 + n)
     states = scenarios.perturbed_states(n, B, rng)
     acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
