@@ -990,11 +990,12 @@ constexpr int DD_ES = 7, DD_RS = 5;
 // k_dd per-wavefront area: with a forest the env rows' LDS image; without one nothing (n = 6:
 // 27.0 KB, four wavefronts per CU -- the unused 20 KB image used to hold k_dd at three, C3 A/B
 // 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers (RowLds measured 26.2 ms).
-// Without a forest the 3 base rows' IPM state (s, z pairs and zw) lives in this area instead (RowLds):
-// with the pair layout it removes the DD agent QP's scratch spills (probe: 52 scratch ops -> 0 per
-// IPM pass for 60 more LDS reads).
+// DAT_DD_ROWLDS: without a forest the 3 base rows' IPM state (s, z pairs and zw) would live in this area
+// instead (RowLds).  It removes the DD agent QP's scratch spills (probe: 52 scratch ops -> 0 per IPM
+// pass for 60 more LDS reads) but measured no gain on C3 (A/B, two runs each: 18.5 / 20.4 ms k_dd with
+// the rows in registers, 21.0 / 20.2 ms in LDS; run-to-run spread ~1 ms), so it is off.
 #ifndef DAT_DD_ROWLDS
-#define DAT_DD_ROWLDS 1
+#define DAT_DD_ROWLDS 0
 #endif
 __host__ __device__ constexpr int dd_area_doubles(bool env) {
   return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE) : 0);
