@@ -523,10 +523,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }
     }
     // ---- one ADMM pass of every occupied slot
+    DAT_PHASE(14);
     const bool active = slot_sc >= 0;
     int it_lane = 0;
     if (active) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho, RT_STRIDE);
+      DAT_PHASE(15);
       P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
       double y[1][3], w[6];
       IPMOut o;

@@ -19,8 +19,8 @@ from distributed_aerial_transportation_amd import _lib as L  # noqa: E402
 NAMES = {0: "ipm init", 1: "residuals + stop test", 2: "NT scaling + D", 3: "M, chol, T, N, P", 4: "predictor newton",
          5: "affine step / gap / sigma", 6: "corrector newton (+refinement)", 7: "step, backtrack, update",
          8: "exit / best iterate", 9: "drain: after the solve (lane results)", 10: "(whole ipm_solve, drain's view)",
-         11: "drain: slot refill + build_shared", 12: "drain: lane setup, env rows, QP data",
-         13: "drain: consensus, dual update, outputs"}
+         11: "drain: slot refill + build_shared", 12: "drain: fresh slot: lane statics, env rows",
+         13: "drain: consensus, dual update, outputs", 14: "drain: lane_cadmm_dynamic", 15: "drain: tuned flag, ipm call"}
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C4")
 ap.add_argument("--steps", type=int, default=4)
