@@ -122,6 +122,13 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
 
 extern "C" {
 
+#if defined(DAT_IPM_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+void datcpu_ipm_stats(long long* out) {
+  for (int k = 0; k < 16; ++k) { out[k] = dat::g_ipm_stats[k]; dat::g_ipm_stats[k] = 0; }
+  for (int k = 0; k < 72; ++k) { out[16 + k] = dat::g_ipm_hist[k / 24][k % 24]; dat::g_ipm_hist[k / 24][k % 24] = 0; }
+}
+#endif
+
 void* datcpu_create(int n, int B, const double* params) {
   if (n < 3 || n > NMAXC || B < 1 || !params) return nullptr;
   Ctx* c = new Ctx();

@@ -592,6 +592,25 @@ struct PhaseClock {
 #define DAT_PHASE(c)
 #endif
 
+// Refinement statistics (host builds with -DDAT_IPM_STATS only, tools/ipm_stats.py): corrector solves,
+// refinement passes run, passes skipped by the rounding-level test.
+#if defined(DAT_IPM_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+inline long long g_ipm_stats[16];  // [0..2] refinement, [3 + why] non-converged exits, [10] in-band, [11] solves
+inline long long g_ipm_hist[3][24];  // [first pass stopped at rounding | correction applied | 2nd pass][log10 max row z/s + 12]
+inline double g_maxw;
+#define DAT_STAT(k) (++g_ipm_stats[k])
+#define DAT_STAT_W(w) (g_maxw = (w) > g_maxw ? (w) : g_maxw)
+#define DAT_STAT_H(k)                                                                   \
+  do {                                                                                  \
+    int b_ = g_maxw > 0 ? (int)floor(log10(g_maxw)) + 12 : 0;                           \
+    ++g_ipm_hist[k][b_ < 0 ? 0 : b_ > 23 ? 23 : b_];                                    \
+  } while (0)
+#else
+#define DAT_STAT(k) ((void)0)
+#define DAT_STAT_W(w) ((void)0)
+#define DAT_STAT_H(k) ((void)0)
+#endif
+
 struct IPMOut {
   int status;
   int iters;
@@ -1001,6 +1020,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 
     // ------------- NT scaling of the cone blocks
     DAT_PHASE(2);
+#if defined(DAT_IPM_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+    g_maxw = 0.0;
+#endif
     SocScale S1[NB], S2[NB];
     bool okc = true;
 #pragma unroll
@@ -1079,6 +1101,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           double sl, zl;
           rst.sz(l, sl, zl);
           const double wgt = zl * frcp(sl);
+          DAT_STAT_W(act(l) * wgt);
           double* X = l < NWROW ? Xw : Xv;
           double a3v[3];
           ra3(l, a3v);
@@ -1307,9 +1330,15 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       }
       // the affine (predictor) direction only sets the step length, sigma and the corrector's
       // second-order term: it is used unrefined; the corrector -- the step actually taken -- is refined
+      // (a gate skipping the pass when every row's barrier weight z/s < 1 -- tools/ipm_stats.py: no
+      // correction was ever applied below z/s = 10 on the C4 loop -- measured slower: C4 k_cadmm 3.74 ->
+      // 4.00 ms, the extra live value costs more than the skipped residual)
       const int nref = corr ? NREF : 0;
+      if (corr) DAT_STAT(0);
 #pragma unroll 1
       for (int ref = 0; ref < nref; ++ref) {
+        DAT_STAT(1);
+        if (ref == 1) DAT_STAT_H(2);
         // linearised dual residual of the full system at (dy, dw); refine
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
@@ -1370,7 +1399,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #ifndef DAT_IPM_REF_THRESH
 #define DAT_IPM_REF_THRESH 1e-12
 #endif
-          if (en <= DAT_IPM_REF_THRESH * sc) break;
+          if (en <= DAT_IPM_REF_THRESH * sc) {
+            DAT_STAT(2);
+            if (ref == 0) DAT_STAT_H(0);
+            break;
+          }
+          if (ref == 0) DAT_STAT_H(1);
         }
 #endif
         core(ek, ef, nullptr, false, true, dy, dwv, du);
@@ -1534,6 +1568,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     }
   }
   DAT_PHASE(8);
+  DAT_STAT(3 + (out.why < 7 ? out.why : 6));
   // not converged to tol: return the best iterate seen; "optimal" if its scaled primal / dual
   // residuals are within north_star's 1e-7 and its complementarity gap within 1e-6 (strongly graded
   // problems -- the rigid payload's Jl^-1 ~ 50 -- can stall at a 1e-7 gap while the structured Newton
