@@ -993,14 +993,19 @@ constexpr int DD_ES = 7, DD_RS = 5;
 // 27.0 KB, four wavefronts per CU -- the unused 20 KB image used to hold k_dd at three, C3 A/B
 // 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers (RowLds measured 26.2 ms).
 // DAT_DD_ROWLDS: without a forest the 3 base rows' IPM state (s, z pairs and zw) would live in this area
-// instead (RowLds).  It removes the DD agent QP's scratch spills (probe: 52 scratch ops -> 0 per IPM
-// pass for 60 more LDS reads) but measured no gain on C3 (A/B, two runs each: 18.5 / 20.4 ms k_dd with
-// the rows in registers, 21.0 / 20.2 ms in LDS; run-to-run spread ~1 ms), so it is off.
+// instead (RowLds), optionally with aux slots (DAT_DD_AUXM).  It removes the DD agent QP's scratch
+// spills (probe: 52 scratch ops -> 0 per IPM pass for 60 more LDS reads) but measured no gain on C3
+// (A/B, two runs each, k_dd ms: rows in registers 18.5 / 20.4, rows in LDS 21.0 / 20.2; again 19.0 /
+// 19.5 against rows + lambda slots 19.8 / 19.7 and rows + scales + lambda 20.4 / 21.4; run-to-run
+// spread ~1 ms), so it is off.
 #ifndef DAT_DD_ROWLDS
 #define DAT_DD_ROWLDS 0
 #endif
+#ifndef DAT_DD_AUXM
+#define DAT_DD_AUXM 0
+#endif
 __host__ __device__ constexpr int dd_area_doubles(bool env) {
-  return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE) : 0);
+  return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE, ipm_aux_doubles(1, DAT_DD_AUXM)) : 0);
 }
 // k_dd_key: drain-order key of every scenario (previous step's DD iteration count, longest first),
 // sorted by k_bucket into one queue (class 0).
@@ -1122,8 +1127,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                        IPM_TOL);
       else if constexpr (DAT_DD_ROWLDS)
-        o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                         IPM_TOL, RowLds{envs, lane});
+        o = ipm_solve<MODE_DD, 1, NBASE, LdsRef<QPShared>, EnvLds, RtLds, RowLds, DAT_DD_AUXM>(
+            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL, RowLds{envs, lane});
       else
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                          IPM_TOL);
