@@ -1007,11 +1007,13 @@ constexpr int DD_ES = 7, DD_RS = 5;
 __host__ __device__ constexpr int dd_area_doubles(bool env) {
   return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE, ipm_aux_doubles(1, DAT_DD_AUXM)) : 0);
 }
-// k_dd_key: drain-order key of every scenario (previous step's DD iteration count, longest first),
-// sorted by k_bucket into one queue (class 0).
+// k_dd_key: drain-order key of every scenario -- the previous step's (DD iteration count, slowest agent
+// QP's IPM iterations), longest first, as k_cadmm's key -- sorted by k_bucket into one queue (class 0).
+// DD agent QPs run the conservative IPM start (9-10 iterations on average): bins <= 8, 9-10, 11-13, >= 14.
+__host__ __device__ inline int dd_ipm_bin(int it) { return it <= 8 ? 0 : it <= 10 ? 1 : it <= 13 ? 2 : 3; }
 __global__ void k_dd_key(KArgs a) {
   const int sc = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sc < a.B) a.need[sc] = NIB - 1 - NPB * iter_bin(a.iters[sc]);
+  if (sc < a.B) a.need[sc] = NIB - 1 - (NPB * iter_bin(a.iters[sc]) + dd_ipm_bin(a.ipmx[sc]));
 }
 
 // DD control step (control/rqp_dd.py:695-752), persistent: each 64-lane block holds G = floor(64/n)
@@ -1038,6 +1040,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* envs = (double*)(shs + G);              // EnvLds image (ENV only)
   int* sid = (int*)(envs + dd_area_doubles(ENV));  // G: scenario of the slot (-1 empty, -2 retired)
   int* done = sid + 64;                           // G: the slot's scenario stopped in this pass
+  int* wmx = done + 64;                           // G: IPM iterations of the slot's slowest agent QP this step
   QPShared& S = shs[lsc];
   double* myX = X + lane * 9;
   double* lF = lamF + lsc * N3;
@@ -1064,6 +1067,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       const int q = atomicAdd(a.qhead, 1);
       sid[ls] = q < cnt ? a.slist[first + q] : -2;
       done[ls] = 0;
+      wmx[ls] = 0;
     }
     __syncthreads();
     const int slot_sc = lane < NT ? sid[ls] : -2;
@@ -1135,6 +1139,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       my_ipm += o.iters;
       my_inband += o.inband;
       my_loose += inband_loose(o);
+      atomicMax(&wmx[ls], o.iters);
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
@@ -1217,6 +1222,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         a.qstatus[(size_t)sc * n + i] = qstat;
         if (i == 0) {
           a.iters[sc] = iter;
+          a.ipmx[sc] = wmx[ls];
           int coll = 0;
           double md = prm[DAT_P_VISR];
           for (int k = 0; k < n; ++k) {
@@ -1696,7 +1702,7 @@ size_t dd_lds(int n, bool env) {
   int G = 64 / n, NT = G * n;
   return sizeof(double) * (al2((size_t)NT * 9) + 2 * al2((size_t)G * 3 * n) + al2((size_t)NT * DD_ES) +
                            (size_t)G * RT_STRIDE * n + 64 * DD_RS) +
-         sizeof(QPShared) * (size_t)G + sizeof(double) * dd_area_doubles(env) + sizeof(int) * 128;
+         sizeof(QPShared) * (size_t)G + sizeof(double) * dd_area_doubles(env) + sizeof(int) * 192;
 }
 size_t dd_setup_lds(int n) {
   int N = 6 * n;
@@ -1857,6 +1863,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->clam, B * n * N3);
   } else if (c.mode == DAT_MODE_DD) {
     rc |= dalloc(h, &h->need, B);
+    rc |= dalloc(h, &h->ipmx, B);
     rc |= dalloc(h, &h->slist, B);
     rc |= dalloc(h, &h->scount, 3 * NCLS);
     rc |= dalloc(h, &h->dlamF, B * N3);
