@@ -48,6 +48,18 @@ constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton so
 #endif
 // divergence stop (from the 5th iteration): merit above DAT_IPM_DIVERGE x the best seen.  A start
 // close to the boundary can raise the residuals by 1e3 in its first steps on a well-posed DD QP.
+// DD agent QPs: the conservative start.  Development knobs; round-3 A/B on C3 (IPM it/QP, ms per step
+// against 9.46, 20.3 / 20.7): S0 = Z0 = 0.3 -> 9.00, 21.4; 0.1 -> 8.89, 22.0; ETA 0.995 -> 9.29, 20.9;
+// 0.1 and 0.995 -> 8.71, 21.8 -- fewer iterations on average, a wider spread across a wavefront.
+#ifndef DAT_DD_S0
+#define DAT_DD_S0 1.0
+#endif
+#ifndef DAT_DD_Z0
+#define DAT_DD_Z0 1.0
+#endif
+#ifndef DAT_DD_ETA
+#define DAT_DD_ETA 0.99
+#endif
 #ifndef DAT_IPM_ETA
 #define DAT_IPM_ETA 0.999  // fraction of the step to the cone boundary (7.00 -> 5.23 -> 4.28 it/QP)
 #endif
@@ -835,9 +847,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   // step), DD agent QPs (C3 29 -> 39 ms) and the centralized QP (also the rigid payload on the same
   // kernel, whose Jl^-1 ~ 50 grades the Newton systems)
   const bool TUNED = MODE == MODE_CADMM && P.tuned;
-  const double S0 = TUNED ? DAT_IPM_S0 : 1.0;
-  const double Z0 = TUNED ? DAT_IPM_Z0 : 1.0;
-  const double ETA = TUNED ? DAT_IPM_ETA : 0.99;
+  const double S0 = TUNED ? DAT_IPM_S0 : MODE == MODE_DD ? DAT_DD_S0 : 1.0;
+  const double Z0 = TUNED ? DAT_IPM_Z0 : MODE == MODE_DD ? DAT_DD_Z0 : 1.0;
+  const double ETA = TUNED ? DAT_IPM_ETA : MODE == MODE_DD ? DAT_DD_ETA : 0.99;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
 #pragma unroll
