@@ -551,6 +551,9 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       DAT_PHASE(9);
       wc.ipm += o.iters;
       wc.inband += o.inband;
+#ifdef DAT_ITER_HIST
+      atomicAdd(&g_iter_hist[o.iters < 63 ? o.iters : 63], 1ull);
+#endif
       wc.loose += inband_loose(o);
       it_lane = o.iters;
       wc.rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
@@ -1140,6 +1143,9 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       my_inband += o.inband;
       my_loose += inband_loose(o);
       atomicMax(&wmx[ls], o.iters);
+#ifdef DAT_ITER_HIST
+      atomicAdd(&g_iter_hist[o.iters < 63 ? o.iters : 63], 1ull);
+#endif
       my_rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++my_qp;
       qstat = o.status;
@@ -1774,6 +1780,15 @@ int finish_hl(dat_handle* h) {
 
 extern "C" {
 
+#ifdef DAT_ITER_HIST
+int dat_get_iter_hist(unsigned long long* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dat::g_iter_hist), sizeof(unsigned long long) * 64));
+  unsigned long long z[64] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(dat::g_iter_hist), z, sizeof(z)));
+  return 0;
+}
+#endif
 #ifdef DAT_PHASE_PROF
 // development builds only (tools/phase_prof.py): the IPM phase cycle sums, reset after the read
 int dat_get_phase_cycles(unsigned long long* out) {

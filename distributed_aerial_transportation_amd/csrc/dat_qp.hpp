@@ -584,6 +584,10 @@ __host__ __device__ constexpr int row_lds_doubles(int NR, int NX = 0) { return (
 #if defined(DAT_PHASE_PROF)
 __device__ unsigned long long g_phase[16];
 #endif
+#if defined(DAT_ITER_HIST)
+// IPM iteration histogram of the agent QPs (development builds, tools/iter_hist.py): [iters] solves
+__device__ unsigned long long g_iter_hist[64];
+#endif
 #if defined(DAT_PHASE_PROF) && defined(__HIP_DEVICE_COMPILE__)
 struct PhaseClock {
   unsigned long long t0;
