@@ -76,6 +76,9 @@ def parse():
                          "QP-level configs (n, mode, batch and parameters follow the config unless given)")
     ap.add_argument("--fixed-work", action="store_true",
                     help="C2/C5 mode (ii): tol 0, 25 ADMM iterations (test/control/test_rqpcontrollers.py:106-110)")
+    ap.add_argument("--qp-tol", type=float, default=1e-10,
+                    help="IPM stopping tolerance of the QPs (default 1e-10; 1e-8 = Clarabel's default, which "
+                         "the reference runs with)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--selftest", action="store_true",
@@ -365,6 +368,7 @@ def main():
 
         scen_forest, states, forests = bench_states(n, B, rank, world, args.forests, args.start, total)
         eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
+        eng.set_qp_tolerance(args.qp_tol)
         eng.set_forests(forests, scen_forest)
         eng.set_state(states, np.zeros(B, dtype=np.int32))
     eng.closed_loop(args.warmup)
@@ -446,7 +450,7 @@ def main():
                  f"synthetic (seeded forests 0..63, randomized C4 {args.start} start states)"),
         "config": {"workload": workload,
                    "n": n, "scenarios_per_gpu": B, "total_scenarios": scen_all, "hl_every": 10, "dt": 1e-3,
-                   "parallelism": f"scenario-sharded x{world}"},
+                   "qp_tol": args.qp_tol, "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
                   "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
@@ -460,7 +464,8 @@ def main():
                      "flops_per_launch": flops_launch,
                      "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"},
     }
-    if not args.no_cpu_baseline and world == 1 and not args.selftest:
+    # (the CPU restatement solves at the default 1e-10: no work-matched baseline at another --qp-tol)
+    if not args.no_cpu_baseline and world == 1 and not args.selftest and args.qp_tol == 1e-10:
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start, args.forests, args.warmup, args.steps, B)
     print(json.dumps(out), flush=True)
     if dist is not None:
@@ -479,6 +484,7 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     states, accs, params, per_scen = qp_level_inputs(cfg, n, B, rng)
     eng = BatchedController(args.mode, n, B, params, per_scenario_params=per_scen,
                             device=local if world > 1 else 0)
+    eng.set_qp_tolerance(args.qp_tol)
     if args.fixed_work:
         eng.set_force_err_tolerance(0.0, False)
         eng.set_max_iter(25)
@@ -544,7 +550,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (perturbed rest states, acc_des ~ U(-5,5)^6" + (", randomized payload mass/inertia)" if per_scen else ")"),
-        "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "parallelism": f"scenario-sharded x{world}"},
+        "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "qp_tol": args.qp_tol,
+                   "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
                   "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
                   "kernel_ms_per_step": step_ms, "inband_exits": int(w.get("inband_exits", 0)),
@@ -555,7 +562,7 @@ def qp_level(args, dist, rank: int, world: int, local: int):
                      "flop_model": f"{fixed:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"
                                    + (" (DD agent QP; dual ascent not counted)" if args.mode == "dd" else "")},
     }
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and args.qp_tol == 1e-10:
         out["cpu_baseline"] = cpu_baseline_qp(cfg, n, args.mode, args.cpu_sample_s, args.fixed_work)
     print(json.dumps(out), flush=True)
     if dist is not None:

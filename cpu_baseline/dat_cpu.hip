@@ -23,6 +23,10 @@
 
 using namespace dat;
 
+#if defined(DAT_IPM_STATS)
+long long g_ith[2][8][32];  // tools/ipm_stats.py: IPM iterations by start and active env rows
+#endif
+
 namespace {
 constexpr int NMAXC = 16;
 
@@ -82,6 +86,9 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
                                                RtPtr{Rt_all + 9 * i}, P[i], feq + 3 * i, y, w, best, 50, 1e-10);
       ++*qp;
       *ipm += o.iters;
+#if defined(DAT_IPM_STATS)
+      ++g_ith[P[i].tuned ? 1 : 0][__builtin_popcount(P[i].emask) & 7][o.iters < 31 ? o.iters : 31];
+#endif
       double* fi = cf + i * N3;
       if (o.status == ST_OPTIMAL) {
         for (int j = 0; j < n; ++j) {
@@ -123,6 +130,10 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
 extern "C" {
 
 #if defined(DAT_IPM_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+void datcpu_ipm_ith(long long* out) {  // [tuned start][active env rows][IPM iterations] solves
+  long long* g = &g_ith[0][0][0];
+  for (int k = 0; k < 512; ++k) { out[k] = g[k]; g[k] = 0; }
+}
 void datcpu_ipm_stats(long long* out) {
   for (int k = 0; k < 16; ++k) { out[k] = dat::g_ipm_stats[k]; dat::g_ipm_stats[k] = 0; }
   for (int k = 0; k < 72; ++k) { out[16 + k] = dat::g_ipm_hist[k / 24][k % 24]; dat::g_ipm_hist[k / 24][k % 24] = 0; }

@@ -110,6 +110,7 @@ EXPORTS = {
     "dat_set_forests": (ctypes.c_int, [H, ctypes.c_int, I, D, I, D]),
     "dat_set_tolerance": (ctypes.c_int, [H, ctypes.c_double, ctypes.c_int]),
     "dat_set_max_iter": (ctypes.c_int, [H, ctypes.c_int]),
+    "dat_set_qp_tolerance": (ctypes.c_int, [H, ctypes.c_double]),
     "dat_reset_warm_start": (ctypes.c_int, [H]),
     "dat_set_state": (ctypes.c_int, [H, D, I]),
     "dat_get_state": (ctypes.c_int, [H, D, I]),

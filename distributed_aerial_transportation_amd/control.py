@@ -126,6 +126,11 @@ class BatchedController:
         L.check(self._lib.dat_set_max_iter(self._h, int(max_iter)))
         self.cfg.max_iter = max_iter
 
+    def set_qp_tolerance(self, tol: float) -> None:
+        """IPM stopping tolerance of every QP (default 1e-10; 1e-8 is Clarabel's default, which the
+        reference runs with: control/rqp_cadmm.py:492). Must lie in [1e-12, 1e-7]."""
+        L.check(self._lib.dat_set_qp_tolerance(self._h, float(tol)))
+
     def set_persistent_blocks(self, blocks: int) -> None:
         """C-ADMM / DD: resident k_cadmm / k_dd workgroups draining the scenario queues (0: default)."""
         L.check(self._lib.dat_set_persistent_blocks(self._h, int(blocks)))

@@ -537,16 +537,16 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
         if (AUXM != 0 && rmode == 2)
           o = ipm_solve<MODE_CADMM, 1, NR, LdsRef<QPShared>, EnvLdsN<NE>, RtLds, RowLds, AUXM>(
-              shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL, RowLds{L.rows, lane});
+              shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane});
         else if (CLS >= ROWLDS_MIN_CLS && rmode == 1)
           o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                           IPM_TOL, RowLds{L.rows, lane});
+                                           a.qp_tol, RowLds{L.rows, lane});
         else
           o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                           IPM_TOL);
+                                           a.qp_tol);
       } else {
         o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                         IPM_TOL);
+                                         a.qp_tol);
       }
       DAT_PHASE(9);
       wc.ipm += o.iters;
@@ -1132,13 +1132,13 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       IPMOut o;
       if constexpr (ENV)
         o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                       IPM_TOL);
+                                       a.qp_tol);
       else if constexpr (DAT_DD_ROWLDS)
         o = ipm_solve<MODE_DD, 1, NBASE, LdsRef<QPShared>, EnvLds, RtLds, RowLds, DAT_DD_AUXM>(
-            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, IPM_TOL, RowLds{envs, lane});
+            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{envs, lane});
       else
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                         IPM_TOL);
+                                         a.qp_tol);
       my_ipm += o.iters;
       my_inband += o.inband;
       my_loose += inband_loose(o);
@@ -1552,9 +1552,9 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
   const RtPtr rtr{Rt_all + 9 * i};
   double* bst = q.best + (size_t)k * best_size(1);
   IPMOut o = dd ? ipm_solve_rows<MODE_DD, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                             IPM_TOL)
+                                             a.qp_tol)
                 : ipm_solve_rows<MODE_CADMM, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
-                                                IPM_MAX_ITER, IPM_TOL);
+                                                IPM_MAX_ITER, a.qp_tol);
   if (dd) {
     double* xo = q.x + (size_t)k * 9;
     for (int c = 0; c < 3; ++c) xo[c] = y[0][c];
@@ -1590,6 +1590,7 @@ struct dat_handle {
   hipEvent_t ek = nullptr;       // C-ADMM: after k_bucket
   double cadmm_ms = 0.0;         // summed device time of k_cadmm
   int persistent_blocks = 1024;  // C-ADMM: resident k_cadmm blocks (CUs x 4 wavefronts)
+  double qp_tol = IPM_TOL;       // IPM stopping tolerance (dat_set_qp_tolerance)
   double* params = nullptr;
   int ppp = 0;
   bool have_params = false;
@@ -1678,6 +1679,7 @@ KArgs kargs(dat_handle* h) {
   a.tau = c.tau_incr;
   a.rho_max = c.rho_max;
   a.record_err = c.record_err;
+  a.qp_tol = h->qp_tol;
   a.cf = h->cf;
   a.cfbar = h->cfbar;
   a.clam = h->clam;
@@ -1988,6 +1990,13 @@ int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res) {
   if (!h) return fail("null handle");
   h->cfg.res_tol = res_tol;
   h->cfg.use_total_res = use_total_res;
+  return 0;
+}
+
+int dat_set_qp_tolerance(dat_handle* h, double tol) {
+  if (!h) return fail("null handle");
+  if (!(tol >= 1e-12 && tol <= 1e-7)) return fail("dat_set_qp_tolerance: tol must lie in [1e-12, 1e-7]");
+  h->qp_tol = tol;
   return 0;
 }
 

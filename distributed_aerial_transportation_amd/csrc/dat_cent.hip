@@ -46,7 +46,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     double y[NB][3], w[6];
     IPMOut o = ipm_solve_rows<MODE_CENT, NB>(nr, PlainRef<QPShared>{&S}, EnvPlain{&E}, RtPtr{&Rt[0][0]}, P,
                                              prm + DAT_P_FEQ(n), y, w, a.best + (size_t)sc * best_size(NB),
-                                             IPM_MAX_ITER, IPM_TOL);
+                                             IPM_MAX_ITER, a.qp_tol);
     q = 1;
     ip = o.iters;
     ib = o.inband;

@@ -12,7 +12,7 @@ constexpr int IPM_MAX_ITER = 50;
 #ifndef DAT_IPM_TOL
 #define DAT_IPM_TOL 1e-10
 #endif
-constexpr double IPM_TOL = DAT_IPM_TOL;
+constexpr double IPM_TOL = DAT_IPM_TOL;  // default IPM stopping tolerance (dat_set_qp_tolerance)
 // C-ADMM env classes (cadmm_block<C>): 0 no env row, then the largest per-agent env-row count of the
 // scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
 constexpr int NCLS = 4;
@@ -22,7 +22,10 @@ __host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c 
 // ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
 // tail of the whole launch)
 constexpr int NAB = 8;   // ADMM / DD iteration bins
-constexpr int NPB = 4;   // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
+#ifndef DAT_IPM_BINS
+#define DAT_IPM_BINS 4
+#endif
+constexpr int NPB = DAT_IPM_BINS;  // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
 constexpr int NIB = NAB * NPB;
 __host__ __device__ inline int iter_bin(int it) {
   if (it <= 3) return it < 1 ? 0 : it - 1;
@@ -30,7 +33,11 @@ __host__ __device__ inline int iter_bin(int it) {
   return 2 + lg < NAB - 1 ? 2 + lg : NAB - 1;
 }
 // IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8
-__host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
+// (DAT_IPM_BINS 6: <= 4, 5, 6, 7, 8, >= 9)
+__host__ __device__ inline int ipm_bin(int it) {
+  if (NPB == 6) return it <= 4 ? 0 : it >= 9 ? 5 : it - 4;
+  return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3;
+}
 constexpr int NKEY = NCLS * NIB;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
 // QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
@@ -78,6 +85,7 @@ struct KArgs {
                                  //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
   unsigned* emask;               // C-ADMM: [B n] env row mask of the step
   int ll_kind;                   // low-level SO(3) law: LL_PD or LL_SM (dat_set_low_level)
+  double qp_tol;                 // IPM stopping tolerance of every QP (dat_set_qp_tolerance)
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)

@@ -82,6 +82,11 @@ int dat_set_forests(dat_handle* h, int num_forests, const int* tree_offsets, con
                     const int* scenario_forest, const double* mountain);
 /* set_force_err_tolerance: control/rqp_cadmm.py:683-685, control/rqp_dd.py:760-761 */
 int dat_set_tolerance(dat_handle* h, double res_tol, int use_total_res);
+/* Stopping tolerance of every agent / centralized QP's interior-point solve (default 1e-10).  The
+ * reference solves with Clarabel's default settings (prob.solve(solver=CLARABEL), control/rqp_cadmm.py:492,
+ * control/rqp_dd.py:485, control/rqp_centralized.py:440: tol_gap_abs = tol_gap_rel = tol_feas = 1e-8);
+ * 1e-8 here is that tolerance.  tol in [1e-12, 1e-7] (the north_star residual bound), else an error. */
+int dat_set_qp_tolerance(dat_handle* h, double tol);
 /* set_max_iter: control/rqp_cadmm.py:687-688, control/rqp_dd.py:763-764 */
 int dat_set_max_iter(dat_handle* h, int max_iter);
 /* _set_warm_start: control/rqp_cadmm.py:577-580, control/rqp_dd.py:628-632 */

@@ -46,3 +46,17 @@ print("log10(max row z/s) bin: [first refinement pass stopped at rounding, corre
 for b in range(24):
     if h[:, b].any():
         print(f"  1e{b - 12:+d}: {h[0, b]:8d} {h[1, b]:8d} {h[2, b]:8d}")
+L.datcpu_ipm_ith.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
+ith = (ctypes.c_longlong * 512)()
+L.datcpu_ipm_ith(ith)
+c.closed_loop(K, threads=1)
+L.datcpu_ipm_ith(ith)
+H = np.array(list(ith)).reshape(2, 8, 32)
+print(f"IPM iterations by start (tuned / conservative) and active env rows ({K} more HL steps):")
+for t in (1, 0):
+    for e in range(8):
+        row = H[t, e]
+        if row.sum():
+            mean = (row * np.arange(32)).sum() / row.sum()
+            print(f"  {'tuned' if t else 'cons.'} env rows {e}: {int(row.sum()):7d} QPs, mean {mean:.2f}: "
+                  + " ".join(f"{k}:{int(v)}" for k, v in enumerate(row) if v))
