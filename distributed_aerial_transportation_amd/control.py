@@ -323,6 +323,10 @@ class _DropIn:
         err = [e for e in err if e == e]
         return f, SolverStatistics(it, r.gpu_ms * 1e-3, bool(r.collision[0]), float(r.min_env_dist[0]), err)
 
+    def set_qp_tolerance(self, tol: float) -> None:
+        """Extension (no reference counterpart): IPM stopping tolerance, 1e-8 = Clarabel's default."""
+        self._eng.set_qp_tolerance(tol)
+
     def get_force_cone_angle_bound(self) -> float:
         return self.max_f_ang
 
