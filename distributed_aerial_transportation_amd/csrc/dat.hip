@@ -1007,6 +1007,9 @@ constexpr int DD_ES = 7, DD_RS = 5;
 #ifndef DAT_DD_AUXM
 #define DAT_DD_AUXM 0
 #endif
+#ifndef DAT_DD_PRICE_RT
+#define DAT_DD_PRICE_RT 0
+#endif
 __host__ __device__ constexpr int dd_area_doubles(bool env) {
   return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE, ipm_aux_doubles(1, DAT_DD_AUXM)) : 0);
 }
@@ -1064,7 +1067,11 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
   double mdist = 0.0;
   long long my_ipm = 0, my_qp = 0, my_rowit = 0, my_inband = 0, my_loose = 0;
+  // phase marks (DAT_PHASE_PROF builds, tools/phase_prof.py): 11 refill + fresh slot setup, 14 prices,
+  // 10 ipm_solve, 9 result bookkeeping, 13 consensus error, stop test, dual ascent, outputs
+  DAT_PHASE_INIT(11);
   for (;;) {
+    DAT_PHASE(11);
     // ---- refill empty slots from the queue
     if (lane < NT && i == 0 && sid[ls] == -1) {
       const int q = atomicAdd(a.qhead, 1);
@@ -1113,6 +1120,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     }
     const bool active = slot_sc >= 0;
     const int nr = wave_max(active ? rows_needed(P.emask) : NBASE);
+    DAT_PHASE(14);
     if (active) {
       // prices (control/rqp_dd.py:718-722)
       double sF[3] = {0, 0, 0}, sM[3] = {0, 0, 0};
@@ -1120,8 +1128,15 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int c = 0; c < 3; ++c) { sF[c] += lF[3 * k + c]; sM[c] += lM[3 * k + c]; }
       double c9[9], dm[3], rxd[3], Rr[3];
       for (int c = 0; c < 3; ++c) dm[c] = sM[c] - lM[3 * i + c];
+#if DAT_DD_PRICE_RT
+      // R_l (r_i x dm) = -Rt_i' dm with Rt_i = hat(r_i) R_l' (the slot's LDS U-map): no global reads
+      (void)rxd;
+      mtv3(rts + RT_STRIDE * i, dm, Rr);
+      for (int c = 0; c < 3; ++c) Rr[c] = -Rr[c];
+#else
       cross3(prm + DAT_P_RCOM(n) + 3 * i, dm, rxd);
       mv3(Rl, rxd, Rr);
+#endif
       for (int c = 0; c < 3; ++c) {
         c9[c] = -(sF[c] - lF[3 * i + c]) + Rr[c];
         c9[3 + c] = lF[3 * i + c];
@@ -1130,15 +1145,20 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
       IPMOut o;
+      if (DAT_DD_WARM >= 2)
+        for (int r = 0; r < 6; ++r) P.atil[r] = prev[3 + r];
+      const double* y0 = DAT_DD_WARM >= 1 ? prev : prm + DAT_P_FEQ(n) + 3 * i;
+      DAT_PHASE(10);
       if constexpr (ENV)
-        o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+        o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                        a.qp_tol);
       else if constexpr (DAT_DD_ROWLDS)
         o = ipm_solve<MODE_DD, 1, NBASE, LdsRef<QPShared>, EnvLds, RtLds, RowLds, DAT_DD_AUXM>(
-            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{envs, lane});
+            shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{envs, lane});
       else
-        o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
+        o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                          a.qp_tol);
+      DAT_PHASE(9);
       my_ipm += o.iters;
       my_inband += o.inband;
       my_loose += inband_loose(o);
@@ -1166,6 +1186,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int c = 0; c < 3; ++c) prev[6 + c] = -jr[c];
       }
     }
+    DAT_PHASE(13);
     __syncthreads();  // agent 0's fallback above reads X before this pass's writes
     if (active) {
       for (int c = 0; c < 9; ++c) myX[c] = prev[c];
@@ -1205,13 +1226,27 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     if (active) {
       if (!done[ls]) {
         // dual ascent: lambda += H^-1 (A x)   (control/rqp_dd.py:678-693); rows 6i..6i+5
-        const double* Hi = a.dHinv + (size_t)sc * N6 * N6;
-        double stp[6];
-        for (int r = 0; r < 6; ++r) {
-          const double* row = Hi + (size_t)(6 * i + r) * N6;
-          double s = 0.0;
-          for (int c = 0; c < N6; ++c) s += row[c] * E[(ls * n + c / 6) * DD_ES + c % 6];
-          stp[r] = s;
+        // The six rows are read agent block by agent block (18 16-byte loads in flight per block, rows
+        // and blocks 48-byte aligned), each row's sum kept in the original order c = 0 .. 6n-1.
+        const double* Hi = a.dHinv + (size_t)sc * N6 * N6 + (size_t)(6 * i) * N6;
+        double stp[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < n; ++k) {
+          dat_d2 h[6][3];
+#pragma unroll
+          for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) h[r][j] = *(const dat_d2*)(Hi + (size_t)r * N6 + 6 * k + 2 * j);
+          const double* e = E + (ls * n + k) * DD_ES;
+          double ev[6];
+#pragma unroll
+          for (int j = 0; j < 6; ++j) ev[j] = e[j];
+#pragma unroll
+          for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+              stp[r] += h[r][j].x * ev[2 * j];
+              stp[r] += h[r][j].y * ev[2 * j + 1];
+            }
         }
         for (int c = 0; c < 3; ++c) {
           lF[3 * i + c] += stp[c];

@@ -57,6 +57,12 @@ constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton so
 #ifndef DAT_DD_Z0
 #define DAT_DD_Z0 1.0
 #endif
+// DD warm start (A/B knob): 0 the IPM starts from f_eq and w = 0; 1 from the agent's previous (f_i)
+// of the scenario (the last DD pass, or the previous step's solution on a slot's first pass); 2 also
+// w = its previous (F_i, M_i)
+#ifndef DAT_DD_WARM
+#define DAT_DD_WARM 0
+#endif
 #ifndef DAT_DD_ETA
 #define DAT_DD_ETA 0.99
 #endif
@@ -881,9 +887,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   // w = atil (the infeasible start lets the Newton steps restore rho (w - atil) + K_{-i} pi = 0).
   // A consistent start through a 6x6 LU of (rho I + K C) took the same iteration count and held
   // ~1 KB/lane more spill frame (C4 A/B: k_cadmm 8.9 -> 7.7 ms without it).
-  if (MODE == MODE_CADMM) {
+  if (MODE == MODE_CADMM || (MODE == MODE_DD && DAT_DD_WARM >= 2)) {
 #pragma unroll
-    for (int r = 0; r < 6; ++r) w[r] = P.atil[r];
+    for (int r = 0; r < 6; ++r) w[r] = P.atil[r];  // DD: the previous (F_i, M_i) (k_dd, DAT_DD_WARM 2)
   }
   {
     double u[6], dv[3], dw[3];
