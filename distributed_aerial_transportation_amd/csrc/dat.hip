@@ -89,6 +89,11 @@ __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
 // traffic 145 -> 23 ops per IPM pass; A/B on MI355X: C2 12.1 -> 11.0 ms, C5 80.7 -> 73.2 ms per step);
 // classes 1 and 2 none (lambda alone in class 1: C4 3.66 vs 3.67 ms, no gain; class 2's 5 env rows
 // fill the budget).
+// C-ADMM consensus mean and residual read agent-major, the three components of a block together
+// (bitwise equal to the component-major loops; C4 A/B: k_cadmm 3.68 / 3.63 -> 3.57 / 3.54 ms)
+#ifndef DAT_CADMM_BLOCKREAD
+#define DAT_CADMM_BLOCKREAD 1
+#endif
 #ifndef DAT_AUXM0
 #define DAT_AUXM0 15
 #endif
@@ -580,11 +585,22 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       ++iter;
       rho = fmin(rho * a.tau, a.rho_max);
       // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
+#if DAT_CADMM_BLOCKREAD
+      // agent-major: the three components of copy k read together (same per-component order)
+      double s3[3] = {0.0, 0.0, 0.0};
+      for (int k = 0; k < n; ++k) {
+        const double* ck = cfs + k * N3 + 3 * i;
+        const double c0 = ck[0], c1 = ck[1], c2 = ck[2];
+        s3[0] += c0; s3[1] += c1; s3[2] += c2;
+      }
+      for (int c = 0; c < 3; ++c) myred[c] = s3[c] / n;
+#else
       for (int c = 0; c < 3; ++c) {
         double s = 0.0;
         for (int k = 0; k < n; ++k) s += cfs[k * N3 + 3 * i + c];
         myred[c] = s / n;
       }
+#endif
     }
     __syncthreads();
     if (active) {
@@ -594,11 +610,22 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       if (a.use_total_res) {
         double rmax = 0.0;
+#if DAT_CADMM_BLOCKREAD
+        double s3[3] = {0.0, 0.0, 0.0};
+        for (int j = 0; j < n; ++j) {
+          const double m0 = myf[3 * j], m1 = myf[3 * j + 1], m2 = myf[3 * j + 2];
+          s3[0] += fabs(m0 - fb[3 * j]);
+          s3[1] += fabs(m1 - fb[3 * j + 1]);
+          s3[2] += fabs(m2 - fb[3 * j + 2]);
+        }
+        for (int r = 0; r < 3; ++r) rmax = fmax(rmax, s3[r]);
+#else
         for (int r = 0; r < 3; ++r) {
           double s = 0.0;
           for (int j = 0; j < n; ++j) s += fabs(myf[3 * j + r] - fb[3 * j + r]);
           rmax = fmax(rmax, s);
         }
+#endif
         myred[6] = rmax;
       } else {
         // aggregate residual (control/rqp_cadmm.py:602-621): own copy's totals of the others
