@@ -127,12 +127,25 @@ __host__ __device__ inline int cadmm_row_mode(int n, int G, int cls) {
     return 1;
   return 0;
 }
+// ADMM multipliers of a slot's lanes (3n per lane) in LDS for the slot's lifetime, when the class's
+// carve leaves room (A/B knob DAT_CADMM_LAMLDS): the pass's multiplier reads (lane_cadmm_dynamic,
+// free blocks, dual update) then stay on chip; the warm-state array is read when a slot is filled and
+// written when its scenario stops.
+#ifndef DAT_CADMM_LAMLDS
+#define DAT_CADMM_LAMLDS 0
+#endif
+__host__ __device__ inline size_t cadmm_lam_doubles(int n, int G) { return al2((size_t)G * n * 3 * n); }
+__host__ __device__ inline bool cadmm_lam_lds(int n, int G, int cls) {
+  return DAT_CADMM_LAMLDS && cadmm_fixed_bytes(n, G) + sizeof(double) * (cadmm_area_doubles(cls, cadmm_row_mode(n, G, cls)) +
+                                                                         cadmm_lam_doubles(n, G)) <= LDS_WAVE_BUDGET;
+}
 // dynamic LDS of a k_cadmm workgroup: the largest carve of the env classes that can occur (without a
 // forest every scenario is class 0, so the launch needs only that carve and more workgroups fit a CU)
 __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NCLS - 1) {
   size_t m = 0;
   for (int c = 0; c <= max_cls; ++c) {
-    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_row_mode(n, G, c));
+    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * (cadmm_area_doubles(c, cadmm_row_mode(n, G, c)) +
+                                                                 (cadmm_lam_lds(n, G, c) ? cadmm_lam_doubles(n, G) : 0));
     m = b > m ? b : m;
   }
   return m;
@@ -141,6 +154,7 @@ struct CadmmLds {
   double *fbar, *Rt, *red, *rows;
   QPShared* sh;
   double* env;
+  double* lam;  // G n x 3n ADMM multipliers (cadmm_lam_lds), after the env image
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
@@ -157,6 +171,7 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.red = L.rows;
   const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
+  L.lam = L.env + env_lds_doubles(class_env_rows(cls));
   return L;
 }
 
@@ -455,6 +470,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   if (cnt == 0) return;
   const int rmode = cadmm_row_mode(n, G, CLS);  // wave-uniform
   CadmmLds L = cadmm_carve(smem, n, G, CLS, rmode);
+  const bool lam_lds = cadmm_lam_lds(n, G, CLS);  // wave-uniform
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * RT_STRIDE * n;
   double* myred = L.red + lane * RDS;
@@ -496,6 +512,11 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       lam = a.clam + ((size_t)sc * n + i) * N3;
+      if (lam_lds) {
+        double* ll = L.lam + (size_t)lane * N3;
+        for (int c = 0; c < N3; ++c) ll[c] = lam[c];
+        lam = ll;
+      }
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
       bst = a.best + ((size_t)sc * n + i) * best_size(1);
@@ -678,6 +699,10 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
         }
         a.qstatus[(size_t)sc * n + i] = qstat;
+        if (lam_lds) {  // the warm multipliers back to the warm-state array
+          double* lg = a.clam + ((size_t)sc * n + i) * N3;
+          for (int c = 0; c < N3; ++c) lg[c] = lam[c];
+        }
         if (i == 0) {
           a.iters[sc] = iter;
           a.ipmx[sc] = L.wmx[ls];
