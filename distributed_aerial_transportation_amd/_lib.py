@@ -63,29 +63,59 @@ def source_hash() -> str:
 STAMP = LIB_PATH + ".srchash"
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile libdat.so (gfx950) next to this file unless it exists and was built from the current
-    sources (content hash, not file times: a copied tree keeps its stamp)."""
-    want = source_hash()
-    have = None
+def _stamp() -> str | None:
     if os.path.exists(LIB_PATH) and os.path.exists(STAMP):
         with open(STAMP) as f:
-            have = f.read().strip()
-    if force or have != want:
-        os.makedirs(OBJ_DIR, exist_ok=True)
-        objs = [os.path.join(OBJ_DIR, os.path.basename(src) + ".o") for src in (SRC, SRC_CENT)]
+            return f.read().strip()
+    return None
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libdat.so (gfx950) next to this file unless it exists and was built from the current
+    sources (content hash, not file times: a copied tree keeps its stamp).  Concurrent callers (the
+    ranks bench.py spawns) serialise on a file lock; objects go to per-process names and the library
+    is moved into place atomically, so a process that loads it never sees a partial file."""
+    import fcntl
+
+    want = source_hash()
+    if not force and _stamp() == want:
+        return LIB_PATH
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    with open(os.path.join(OBJ_DIR, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and _stamp() == want:  # built by another process while this one waited
+            return LIB_PATH
+        tag = f"{os.getpid()}"
+        objs = [os.path.join(OBJ_DIR, f"{os.path.basename(src)}.{tag}.o") for src in (SRC, SRC_CENT)]
+        tmp_lib = f"{LIB_PATH}.{tag}.tmp"
         cmds = [["hipcc"] + HIPFLAGS + ["-c", src, "-o", o] for src, o in zip((SRC, SRC_CENT), objs)]
         procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for c in cmds]
-        for c, pr in zip(cmds, procs):
-            _, err = pr.communicate()
-            if pr.returncode != 0:
-                raise DatError("hipcc failed: " + " ".join(c) + "\n" + err[-4000:])
-        link = ["hipcc"] + HIPFLAGS + ["-shared"] + objs + ["-o", LIB_PATH]
-        r = subprocess.run(link, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise DatError("hipcc link failed:\n" + r.stderr[-4000:])
-        with open(STAMP, "w") as f:
-            f.write(want + "\n")
+        errs = []
+        try:
+            for c, pr in zip(cmds, procs):
+                _, err = pr.communicate()
+                if pr.returncode != 0:
+                    errs.append("hipcc failed: " + " ".join(c) + "\n" + err[-4000:])
+        finally:
+            for pr in procs:  # never leave a compiler behind
+                if pr.poll() is None:
+                    pr.kill()
+                    pr.wait()
+        try:
+            if errs:
+                raise DatError("\n".join(errs))
+            link = ["hipcc"] + HIPFLAGS + ["-shared"] + objs + ["-o", tmp_lib]
+            r = subprocess.run(link, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise DatError("hipcc link failed:\n" + r.stderr[-4000:])
+            os.replace(tmp_lib, LIB_PATH)
+            with open(STAMP + f".{tag}", "w") as f:
+                f.write(want + "\n")
+            os.replace(STAMP + f".{tag}", STAMP)
+        finally:
+            for o in objs + [tmp_lib]:
+                if os.path.exists(o):
+                    os.remove(o)
         if verbose:
             for c in cmds + [link]:
                 print(" ".join(c))

@@ -395,16 +395,18 @@ class _PrimalSolver:
 class RQPCADMMPrimalSolver(_PrimalSolver):
     """control/rqp_cadmm.py:26-507: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) ->
     (f (3, n), solve_time, collision, min_env_dist).  Exception -> f_eq (:491-494); non-OPTIMAL ->
-    previous solution (:496-499).  cadmm_rho must be > 0: the reference's default 0 (:487) is its
-    constructor's warm-up solve (:131-140), at which the copies f_j, j != i, are not unique (that solve
-    only seeds Clarabel's warm start); rho <= 0 raises ValueError instead of silently solving another QP."""
+    previous solution (:496-499).  Difference from the reference: cadmm_rho defaults to 1.0 (the
+    controller's rho0, control/rqp_cadmm.py:556-567) instead of 0 (:487).  The reference calls rho = 0 only
+    in its constructor's warm-up solve (:131-140), where the copies f_j, j != i, are not unique (that solve
+    only seeds Clarabel's warm start); an explicit rho <= 0 raises ValueError instead of silently solving
+    another QP."""
 
     _mode = L.MODE_CADMM
 
     def _set_warm_start(self) -> None:
         self.prev_f = self.f_eq.copy()
 
-    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 0, f_mean=None):
+    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 1.0, f_mean=None):
         n = self.n
         if not float(cadmm_rho) > 0.0:
             raise ValueError(f"cadmm_rho must be > 0 (got {cadmm_rho}): at rho = 0 the agent QP's copies f_j, "

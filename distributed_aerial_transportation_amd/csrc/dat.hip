@@ -1658,6 +1658,9 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
       }
     }
   }
+  // in-band accepts (rare: per lane, no wavefront reduction)
+  if (o.inband) atomicAdd(a.counters + CNT_INBAND, 1);
+  if (inband_loose(o)) atomicAdd(a.counters + CNT_INBAND + 1, 1);
   q.status[k] = o.status;
   q.iters[k] = o.iters;
   q.col[k] = (unsigned char)env.collision;

@@ -32,9 +32,14 @@ namespace dat {
 constexpr int NWROW = 2;          // slots [0, NWROW) act on dwl
 constexpr int NBASE = 3;          // base slots shared by all agents of a scenario
 #ifndef DAT_IPM_NREF
-#define DAT_IPM_NREF 2
+#define DAT_IPM_NREF 6
 #endif
-constexpr int NREF = DAT_IPM_NREF;  // iterative-refinement passes per Newton solve
+// iterative-refinement passes per corrector solve (at most; a pass stops the loop once the linearised
+// system is solved to rounding, so well-scaled QPs run one).  Badly scaled agent QPs -- consensus
+// multipliers ~1e3-1e4 in a stalled ADMM loop, active rows with barrier weights z/s ~1e15 -- need up to
+// six to keep the dual residual below the stopping tolerance (tools/hard_qp_probe.py: 2 passes left
+// 281 of 798 such solves at in-band exits, 6 passes 69, all within 1.5e-6 of the oracle)
+constexpr int NREF = DAT_IPM_NREF;
 // Initial point: cone / row slacks shifted to at least DAT_IPM_S0 inside, duals DAT_IPM_Z0 e.  The
 // agent QPs' multipliers are O(1e-2) at the solution; starting the duals and the slack margins there
 // instead of at 1 takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU
@@ -190,6 +195,7 @@ struct QPLane {
   int infeasible;
   int tuned;                     // C-ADMM: first ADMM pass of the step (tuned IPM start, see ipm_solve)
   double kappa, rho, min_fz, max_f, sec;
+  double a2;                     // C-ADMM: sum_{j != i} ||a_j||^2 (objective constant of the free blocks)
   double q[NB][3];               // per-block linear term
   double atil[6];                // C-ADMM: sum_{j != i} U_j a_j
   double cw[6];                  // DD: linear cost on w = (F_i, M_i)
@@ -352,6 +358,7 @@ DAT_HD void lane_common(QPLane<NB>& P, const double* prm) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) { P.atil[r] = 0.0; P.cw[r] = 0.0; }
   P.rho = 1.0;
+  P.a2 = 0.0;
 }
 
 // C-ADMM agent i (control/rqp_cadmm.py:26-501): variables f in R^{3 x n} (agent i's full copy).
@@ -373,6 +380,7 @@ DAT_HD void lane_cadmm_dynamic(QPLane<1>& P, const double* prm, int n, int i, co
   const double* feq = prm + DAT_P_FEQ(n) + 3 * i;
 #pragma unroll
   for (int r = 0; r < 6; ++r) P.atil[r] = 0.0;
+  double a2 = 0.0;
   for (int j = 0; j < n; ++j) {
     double a[3] = {fbar[3 * j] - lam[3 * j] * irho, fbar[3 * j + 1] - lam[3 * j + 1] * irho,
                    fbar[3 * j + 2] - lam[3 * j + 2] * irho};
@@ -384,8 +392,10 @@ DAT_HD void lane_cadmm_dynamic(QPLane<1>& P, const double* prm, int n, int i, co
       U_apply(Rt_all + rt_stride * j, a, t);
 #pragma unroll
       for (int r = 0; r < 6; ++r) P.atil[r] += t[r];
+      a2 += a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
     }
   }
+  P.a2 = a2;
 }
 // agent i's copy of agent j != i: f_j = a_j - U_j' pi / rho  (stationarity of the free blocks)
 DAT_HD void cadmm_free_block(const double* Rt_j, const double* lam_j, const double* fbar_j, const double* pi,
@@ -927,6 +937,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     double dv[3], dw[3];
     double dres = 0.0, pres = 0.0, gap = 0.0;
     double chk = 0.0;  // plain sum of every residual entry: NaN / Inf propagate (fmax drops NaN)
+    // primal objective of the iterate (constants dropped, as cvxpy hands it to the solver): the scale
+    // of the relative gap test
+    double pobj = 0.0;
     {
       double u[6], pi[6], az[6];
       compute_u(u);
@@ -937,7 +950,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         double cu6[6];
         ldn<6>(cup(), cu6);
 #pragma unroll
-        for (int r = 0; r < 6; ++r) pi[r] += cu6[r] - az[r];
+        for (int r = 0; r < 6; ++r) {
+          pobj += u[r] * (0.5 * pi[r] + cu6[r]);
+          pi[r] += cu6[r] - az[r];
+        }
       }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -947,6 +963,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const double r = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
+          pobj += y[k][c] * (0.5 * kap * y[k][c] + P.q[k][c]);
           RK(k, c) = r;
           dres = fmax(dres, fabs(r));
           chk += r;
@@ -955,13 +972,23 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       {
         double Rf[6];
         if (MODE == MODE_CADMM) {
+          // free blocks f_j = a_j - U_j' pi / rho: sum_j rho/2 ||f_j||^2 - rho a_j . f_j
+          //   = pi' K_{-i} pi / (2 rho) - rho/2 sum_j ||a_j||^2
           double kp[6];
           Kmul(pi, kp);
+          double pkp = 0.0;
 #pragma unroll
-          for (int r = 0; r < 6; ++r) Rf[r] = P.rho * (w[r] - P.atil[r]) + kp[r];
+          for (int r = 0; r < 6; ++r) {
+            Rf[r] = P.rho * (w[r] - P.atil[r]) + kp[r];
+            pkp += pi[r] * kp[r];
+          }
+          pobj += 0.5 * (pkp * irho - P.rho * P.a2);
         } else if (MODE == MODE_DD) {
 #pragma unroll
-          for (int r = 0; r < 6; ++r) Rf[r] = pi[r] + P.cw[r];
+          for (int r = 0; r < 6; ++r) {
+            Rf[r] = pi[r] + P.cw[r];
+            pobj += P.cw[r] * w[r];
+          }
         } else {
 #pragma unroll
           for (int r = 0; r < 6; ++r) Rf[r] = 0.0;
@@ -1002,11 +1029,16 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         break;
       }
       const double nh = NH(), nq = NQ();
-      double merit = fmax(fmax(pres / nh, dres / nq), gap);
+      // complementarity gap relative to the objective (Clarabel's gap_rel and the oracle's rule): with
+      // multipliers ~1e3-1e4 (a stalled ADMM loop) an absolute gap below 1e-9 lies under the rounding
+      // floor of s o z, and the Newton systems break down before reaching it
+      const double grel = gap * frcp(fmax(1.0, fabs(pobj)));
+      double merit = fmax(fmax(pres / nh, dres / nq), grel);
 #ifdef DAT_IPM_TRACE
-      printf("ipm it %2d pres %.3e dres %.3e gap %.3e merit %.3e\n", it, pres / nh, dres / nq, gap, merit);
+      printf("ipm it %2d pres %.3e dres %.3e gap %.3e merit %.3e pobj %.3e\n", it, pres / nh, dres / nq, grel, merit,
+             pobj);
 #endif
-      if (pres < tol * nh && dres < tol * nq && gap < 10.0 * tol) {
+      if (pres < tol * nh && dres < tol * nq && grel < 0.1 * tol) {
         out.status = ST_OPTIMAL;
         out.merit = merit;
 #pragma unroll
@@ -1018,7 +1050,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       // ends out of band is INACCURATE and the callers hold their previous solution instead, so
       // out-of-band iterates are never recorded (the record is written in the last one or two
       // iterations of a stalling solve, not at every iteration).
-      const bool band = fmax(pres / nh, dres / nq) < 1e-7 && gap < 1e-6;
+      const bool band = fmax(pres / nh, dres / nq) < 1e-7 && grel < 1e-6;
       if (band && merit < BK()) {
         BK() = merit;
 #pragma unroll
@@ -1420,6 +1452,9 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(RF(r))); }
 #ifndef DAT_IPM_REF_THRESH
 #define DAT_IPM_REF_THRESH 1e-12
+#endif
+#ifdef DAT_IPM_TRACE
+          printf("    ref %d en %.3e sc %.3e\n", ref, en, sc);
 #endif
           if (en <= DAT_IPM_REF_THRESH * sc) {
             DAT_STAT(2);

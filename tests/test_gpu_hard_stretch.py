@@ -2,15 +2,16 @@
 controller itself runs into trouble -- DD's dual ascent climbs 12 -> 59 iterations and stalls at
 max_iter for seven HL steps before recovering (control/rqp_dd.py:695-752); C-ADMM next to a tree stalls
 at max_iter from the 12th step on (control/rqp_cadmm.py:631-675) -- both inside the reference loop of
-example/rqp_example.py:120-131.  The GPU loop (cold warm state, the production kernels) must follow the
-oracle through it: iteration counts exact at every step and f_des within 1e-5 up to the first stalled
-step.  Inside the stall f_des is not compared.  The multipliers grow to ~1e3-1e4 there, and this
-repo's reduced agent-QP IPM breaks down numerically on some of those badly scaled QPs (non-finite or
-divergent iterates) that the oracle's dense IPM solves.  The affected agent then holds its previous
-solution, so the stalled consensus ends elsewhere: on the C-ADMM stretch f_des differs by up to 0.94
-relative at the last step, while the oracle against itself (QP tolerance 1e-10 vs 1e-11) stays within
-1e-6 (known gap).  These are the states where the long-horizon runs (test_gpu_long.py) leave the reference's
-trajectory for good: the failure is the controller's, not the solver's."""
+example/rqp_example.py:120-131.  Inside a stall the consensus multipliers grow to ~1e3-1e4 and the agent
+QPs carry active rows with barrier weights z/s ~1e15 (control/rqp_cadmm.py:482-501,627-629,661); the
+reduced IPM must still solve them to the oracle's accuracy (relative gap test, up to six refinement
+passes per corrector solve: csrc/dat_qp.hpp).
+
+The GPU loop (cold warm state, the production kernels) must follow the oracle through the whole
+stretch: iteration counts exact at every step and f_des within 1e-5 relative at every step.  The DD
+stall is sensitive to solver accuracy in the reference loop itself: the oracle at QP tolerance 1e-10
+against 1e-11 (f_des_1e10 in the fixture) moves f_des by up to 7.6e-5 there, so a DD step is held to
+max(1e-5, 5 x that sensitivity)."""
 
 import numpy as np
 import pytest
@@ -31,19 +32,19 @@ def test_gpu_hard_stretch_matches_oracle(ct, name):
     eng.set_state(d["x0"][None], np.zeros(1, dtype=np.int32))
     its = d["iters"].astype(int)
     stall = int(np.argmax(its > 100))
-    worst = 0.0
+    worst, worst_inside = 0.0, 0.0
     assert stall > 0 and its.max() == 101
     for k in range(K):
         r = eng.control(None, None)
         assert r.iters[0] == its[k], (k, r.iters[0], its[k])
         ref = d["f_des"][k]
-        rel = np.max(np.abs(r.f_des[0] - ref)) / max(1.0, np.max(np.abs(ref)))
-        if k < stall:
-            assert rel < 1e-5, (k, rel)
-        else:
-            # inside the stall only the iteration count is asserted: see the module docstring
-            assert np.all(np.isfinite(r.f_des[0]))
-            worst = max(worst, rel)
+        scale = max(1.0, np.max(np.abs(ref)))
+        rel = np.max(np.abs(r.f_des[0] - ref)) / scale
+        sens = np.max(np.abs(d["f_des_1e10"][k] - ref)) / scale
+        assert rel < max(1e-5, 5.0 * sens), (k, rel, sens)
+        worst = max(worst, rel)
+        if k >= stall:
+            worst_inside = max(worst_inside, rel)
         eng.rollout(10)
-    print(f"{ct}: iteration counts exact over {K} steps, f_des within 1e-5 before the stall (step {stall}); "
-          f"largest f_des difference inside it {worst:.2e}")
+    print(f"{ct}: iteration counts exact over {K} steps; largest f_des difference {worst:.2e} "
+          f"(inside the stall from step {stall}: {worst_inside:.2e})")

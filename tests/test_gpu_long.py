@@ -18,10 +18,9 @@ states at step 2280 (its iteration counts stay identical through step 2300); the
 step 2083, its iteration counts at step 2237 and its states at step 2240.  The GPU run is required to match (f_des 1e-5,
 iteration counts exact, states / x_err / v_err / w / min_env_dist 1e-4) up to that
 reproducibility horizon REPRO_HL (at most the recorded horizon).  Beyond it the test requires the GPU
-run to complete the horizon with finite logs (the centralized run also collision free with mean
-tracking errors within 10 % of the reference's): the distributed controllers can leave the reference's
-trajectory into states where they fail on their own, as the oracle confirms from those very states
-(test_gpu_hard_stretch.py).
+run to complete the horizon with finite logs, collision free, with mean tracking errors within 10 % of
+the reference's: the distributed controllers can leave the reference's trajectory into states where
+their outer loops stall, as the oracle confirms from those very states (test_gpu_hard_stretch.py).
 """
 
 import os
@@ -103,19 +102,17 @@ def test_gpu_long_closed_loop_logs(tag, ct, capsys):
     np.testing.assert_allclose(logs["v_err_seq"][:Hl], d["v_err"][:Hl], rtol=0, atol=1e-4)
     w = np.array([np.concatenate([fw.reshape(-1), Mw.reshape(-1)]) for fw, Mw in logs["w_seq"][::every]])
     np.testing.assert_allclose(w[: H // every], d["w"][: H // every], rtol=0, atol=1e-4)
-    # beyond it the run must complete with finite logs.  Past the horizon the trajectories part for
-    # good, and the distributed controllers can reach states from which they fail on their own: the DD
-    # loop's dual ascent stalls at max_iter from HL ~4316 on, the C-ADMM loop's consensus next to a tree
-    # at ~5606 (rounding-dependent) -- the oracle does exactly the same from those states
-    # (test_gpu_hard_stretch.py) -- and the loop then holds saturated or infeasible agent solutions
-    # (control/rqp_dd.py:490-494, control/rqp_cadmm.py:491-499).  The centralized loop must also stay a
-    # valid closed loop (collision free, mean tracking errors within 10 % of the reference's).
+    # beyond it the run must complete with finite logs and stay a valid closed loop: collision free and
+    # mean tracking errors within 10 % of the reference's.  Past the horizon the trajectories part for
+    # good, and the distributed controllers can reach states where their outer loop stalls at max_iter
+    # (the DD loop's dual ascent, the C-ADMM consensus next to a tree) -- the oracle does exactly the same
+    # from those states (test_gpu_hard_stretch.py, where the GPU also matches the oracle's f_des inside
+    # the stall); a collision or a jump in tracking error there would mean the agent QPs failed.
     assert np.all(np.isfinite(f)) and np.all(np.isfinite(logs["x_err_seq"]))
-    if ct == "centralized":
-        assert min(logs["min_env_dist_seq"]) > 0.0 and min(d["min_dist"]) > 0.0
-        for key in ("x_err", "v_err"):
-            g, r = float(np.mean(logs[key + "_seq"])), float(np.mean(d[key]))
-            assert abs(g - r) <= 0.1 * r, (key, g, r)
+    assert min(logs["min_env_dist_seq"]) > 0.0 and min(d["min_dist"]) > 0.0
+    for key in ("x_err", "v_err"):
+        g, r = float(np.mean(logs[key + "_seq"])), float(np.mean(d[key]))
+        assert abs(g - r) <= 0.1 * r, (key, g, r)
     # the statistics printout of example/rqp_example.py:62-80
     example.print_stats(logs["iter_seq"], logs["solve_time_seq"])
     out = capsys.readouterr().out
