@@ -7,8 +7,9 @@ every scenario, fully on device: forest desired-acceleration law + C-ADMM contro
 rows, up to 101 ADMM iterations of n agent QPs each) + 10 simulation steps (SO(3) PD + dynamics).
 
     python bench.py [--gpus N --steps K --warmup W --batch B --n 6 --mode cadmm]
-    python bench.py --gpus N --total-batch 65536   (strong scaling: BASELINE configs[3], 65,536 scenarios
-                                                   split over the N GPUs; the default is weak scaling)
+    python bench.py --gpus N   (default: strong scaling, BASELINE configs[3]: 65,536 scenarios split over
+                                the N GPUs, the same global scenario set for every N)
+    python bench.py --gpus N --batch 65536   (weak scaling: 65,536 scenarios per GPU)
     python bench.py --config C2|C3|C5 [--fixed-work]   (QP-level configs of SURVEY.md 8(d))
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
@@ -62,10 +63,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=None, help="scenarios per GPU (C4: 65536)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="weak scaling: this many scenarios per GPU (C4 default: strong scaling, see --total-batch)")
     ap.add_argument("--total-batch", type=int, default=None,
-                    help="strong scaling: this many scenarios in total, split over the ranks (BASELINE configs[3]: "
-                         "65536 across 8 GPUs = 8192 per GPU); the same global scenario set for every N")
+                    help="strong scaling: this many scenarios in total, split over the ranks (C4 default when --batch "
+                         "is not given: BASELINE configs[3], 65536 across the GPUs, 8192 per GPU at N = 8); the "
+                         "same global scenario set for every N")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--mode", default=None)
     ap.add_argument("--forests", type=int, default=64)
@@ -87,6 +90,10 @@ def parse():
     n, mode, batch = QP_CONFIGS.get(args.config, (6, "cadmm", 65536))
     args.n = n if args.n is None else args.n
     args.mode = mode if args.mode is None else args.mode
+    if args.config == "C4" and args.batch is None and args.total_batch is None:
+        # the headline measures BASELINE configs[3] at every N: 65,536 scenarios split over the ranks
+        # (N = 1 runs the same 65,536 scenarios as the weak mode's rank 0)
+        args.total_batch = batch
     args.batch = batch if args.batch is None else args.batch
     return args
 

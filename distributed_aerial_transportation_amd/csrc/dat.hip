@@ -9,7 +9,8 @@
 //              (control/rqp_dd.py:513-555, 634-657).
 //   k_dd       DD control step: prices, agent QPs, consensus error, dual ascent through H^-1
 //              (control/rqp_dd.py:659-752).
-//   k_cent     centralized QP, one lane per scenario (control/rqp_centralized.py:436-448): dat_cent.hip.
+//   k_cent     centralized QP, one lane group per scenario and one lane per agent's force
+//              (control/rqp_centralized.py:436-448): dat_cent.hip.
 //   k_rollout_agents  low-level SO(3) law + dynamics + Lie integration, one lane per agent.
 //   k_desired  forest desired-acceleration law (example/rqp_example.py:33-59).
 #include <hip/hip_runtime.h>
@@ -1846,8 +1847,7 @@ int launch_hl(dat_handle* h) {
     else
       hipLaunchKernelGGL(k_dd<false>, dim3(std::min(blocks, h->persistent_blocks)), dim3(64), dd_lds(n, h->nforest > 0), h->stream, a);
   } else {
-    int blocks = (B + 63) / 64;
-    HIPCHK(launch_cent(n, blocks, h->stream, a));
+    HIPCHK(launch_cent(n, B, h->stream, a));
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(h->e1, h->stream));
@@ -1923,7 +1923,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   const dat_config& c = *cfg;
   if (c.n < 3 || c.n > NMAX) return fail("dat_create: n must be in [3, 16]");
   if (c.mode == DAT_MODE_DD && c.n > NMAX_DD) return fail("dat_create: DD supports n <= 16");
-  if (c.mode == DAT_MODE_CENTRALIZED && c.n > NMAX_CENT) return fail("dat_create: centralized supports n <= 6");
+  if (c.mode == DAT_MODE_CENTRALIZED && c.n > NMAX_CENT) return fail("dat_create: centralized supports n <= 16");
   if (c.mode < 0 || c.mode > 2) return fail("dat_create: bad mode");
   if (c.batch < 1) return fail("dat_create: batch must be >= 1");
   if (c.max_iter < 0) return fail("dat_create: max_iter must be >= 0");
@@ -1981,7 +1981,8 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->pf, B * N3);
   }
   // lane-private IPM best-iterate records
-  rc |= dalloc(h, &h->best, c.mode == DAT_MODE_CENTRALIZED ? B * (size_t)best_size(c.n) : B * n * (size_t)best_size(1));
+  // best-iterate records: one per agent QP lane (centralized: one per lane of the scenario's 16-lane slot)
+  rc |= dalloc(h, &h->best, c.mode == DAT_MODE_CENTRALIZED ? B * 16 * (size_t)best_size(1) : B * n * (size_t)best_size(1));
   if (rc) {
     std::string m = g_err;
     dat_destroy(h);

@@ -1,7 +1,16 @@
-// dat_cent.hip -- the centralized QP kernel (control/rqp_centralized.py:27-455), one lane per scenario,
-// instantiated for every team size 3 <= n <= NMAX_CENT.  Its own translation unit: the per-n
-// instantiations of the n-block IPM are compiled in parallel with dat.hip (distributed_aerial_
-// transportation_amd/_lib.py) and linked into libdat.so.
+// dat_cent.hip -- the centralized QP kernel (control/rqp_centralized.py:27-455): one lane group per
+// QP, one lane per agent's force.  Its own translation unit (compiled in parallel with dat.hip by
+// distributed_aerial_transportation_amd/_lib.py and linked into libdat.so).
+//
+// The centralized QP couples the n agents' forces only through the aggregate wrench u = sum_k U_k f_k
+// (DESIGN.md section 2): every cone block's work (residuals, NT scalings, the 3x3 blocks D_k, step
+// lengths) is independent, and the u-space algebra (6x6 Hessians, Cholesky factors, row slots) is
+// shared.  So the QP of one scenario runs on a group of W lanes (W = 4, 8, 16 >= n): lane k holds agent
+// k's block (NB = 1 per lane) and a replica of the u-space algebra; the block sums the u-space algebra
+// needs (u, T = sum_k U_k D_k^-1 U_k', the core solves' right-hand sides, gap, step length, residual
+// norms) are DPP butterflies over the group (GrpDpp, dat_qp.hpp), bit-identical on every lane.  Lanes
+// k >= n of a group are phantoms: they run block 0's data and contribute nothing to any reduction.
+// The per-scenario data (QPShared, the env CBF rows) sit in LDS once per group; each lane's U-map in LDS.
 #include <hip/hip_runtime.h>
 
 #include "dat_kargs.hpp"
@@ -10,57 +19,117 @@ using namespace dat;
 
 namespace {
 
-// ------------------------------------------------------------------------------------------------
-// centralized: one lane per scenario
-// ------------------------------------------------------------------------------------------------
-template <int NB>
+// env CBF rows of one QP shared by a lane group: slot j = (a0, a1, a2, b) at doubles [4 j, 4 j + 3]
+// (two 16-byte pair reads; the group's lanes read the same address: an LDS broadcast)
+struct EnvRec {
+  const volatile DAT_LDS dat_d2* p;
+  __device__ explicit EnvRec(const double* base) : p((const volatile DAT_LDS dat_d2*)base) {}
+  __device__ double b(int j) const { return p[2 * j + 1].y; }
+  __device__ void a3(int j, double* o) const {
+    const dat_d2 f0 = p[2 * j], f1 = p[2 * j + 1];
+    o[0] = f0.x; o[1] = f0.y; o[2] = f1.x;
+  }
+  __device__ void ab(int j, double* o, double& bb) const {
+    const dat_d2 f0 = p[2 * j], f1 = p[2 * j + 1];
+    o[0] = f0.x; o[1] = f0.y; o[2] = f1.x;
+    bb = f1.y;
+  }
+};
+
+template <int W>
+struct CentLds {
+  static constexpr int G = 64 / W;  // QPs (scenarios) per wavefront
+  QPShared sh[G];
+  alignas(16) double env[G][4 * DAT_NENV];
+  alignas(16) double rt[64][RT_STRIDE];
+  int emask[G], infeasible[G];
+};
+
+template <int W, int NR>
+__device__ IPMOut cent_solve(const KArgs& a, CentLds<W>& L, int g, int lane, const QPLane<1>& P, bool active,
+                             const double* y0, double y[1][3], double w[6], double* bst) {
+  return ipm_solve<MODE_CENT, 1, NR, LdsRef<QPShared>, EnvRec, RtLds, RowRegs, 0, GrpDpp<W>>(
+      LdsRef<QPShared>{L.sh, g}, EnvRec{L.env[g]}, RtLds{&L.rt[0][0], lane * RT_STRIDE}, P, y0, y, w, bst,
+      IPM_MAX_ITER, a.qp_tol, RowRegs{}, GrpDpp<W>{active, a.n});
+}
+
+template <int W>
 __global__ __launch_bounds__(64) void k_cent(KArgs a) {
-  const int sc = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = sc < a.B;
-  const int n = NB;
-  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0;
+  __shared__ CentLds<W> L;
+  constexpr int G = CentLds<W>::G;
+  const int lane = threadIdx.x, g = lane / W, k = lane - g * W;
+  const int n = a.n;
+  const int sc = blockIdx.x * G + g;
+  const bool valid = sc < a.B;          // group-uniform
+  const bool active = valid && k < n;   // the lane holds agent k's force
+  const int kk = active ? k : 0;        // phantom lanes run block 0's data
   const double* prm = valid ? prm_of(a, sc) : a.params;
-  QPShared S;
-  QPLane<NB> P;
-  double Rt[NB][9];
-  EnvRows E;
+  const double* st = a.state + (size_t)(valid ? sc : 0) * a.S;
   EnvOut env;
   env.collision = 0;
   env.min_env_dist = 0.0;
+  if (valid) {
+    make_Rt(prm + DAT_P_RCOM(n) + 3 * kk, st + DAT_S_RL(n), L.rt[lane]);
+    if (k == 0) {
+      QPShared& S = L.sh[g];
+      build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
+      const double* trees;
+      int nt;
+      unsigned em;
+      forest_of(a, sc, &trees, &nt);
+      double lhs[DAT_NENV][3], rhs[DAT_NENV];
+      env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &em, lhs, rhs);
+      QPLane<1> P0;
+      EnvRows E;
+      set_env_rows(P0, E, S, em, lhs, rhs);
+      for (int j = 0; j < DAT_NENV; ++j) {
+        L.env[g][4 * j] = E.a[j][0];
+        L.env[g][4 * j + 1] = E.a[j][1];
+        L.env[g][4 * j + 2] = E.a[j][2];
+        L.env[g][4 * j + 3] = E.b[j];
+      }
+      L.emask[g] = (int)P0.emask;
+      L.infeasible[g] = P0.infeasible;
+    }
+  }
+  __syncthreads();
+  QPLane<1> P;
+  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0;
   int nr = NBASE;
   if (valid) {
-    const double* st = a.state + (size_t)sc * a.S;
-    build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFC], prm[DAT_P_KMC], 2, false);
-    lane_cent<NB>(P, prm, n, st, Rt);
-    const double* trees;
-    int nt;
-    unsigned emask;
-    forest_of(a, sc, &trees, &nt);
-    double lhs[DAT_NENV][3], rhs[DAT_NENV];
-    env = env_rows(prm, n, st, trees, nt, -1, prm[DAT_P_AENVC], &emask, lhs, rhs);
-    set_env_rows(P, E, S, emask, lhs, rhs);
+    lane_common(P, prm);
+    P.var = 1;
+    const double kfeq = prm[DAT_P_KFEQ];
+    P.kappa = 2.0 * kfeq;
+    for (int c = 0; c < 3; ++c) P.q[0][c] = -2.0 * kfeq * prm[DAT_P_FEQ(n) + 3 * kk + c];
+    P.emask = (unsigned)L.emask[g];
+    P.infeasible = L.infeasible[g];
     nr = rows_needed(P.emask);
   }
   nr = wave_max(nr);
   if (valid) {
-    double y[NB][3], w[6];
-    IPMOut o = ipm_solve_rows<MODE_CENT, NB>(nr, PlainRef<QPShared>{&S}, EnvPlain{&E}, RtPtr{&Rt[0][0]}, P,
-                                             prm + DAT_P_FEQ(n), y, w, a.best + (size_t)sc * best_size(NB),
-                                             IPM_MAX_ITER, a.qp_tol);
-    q = 1;
-    ip = o.iters;
-    ib = o.inband;
-    lo = inband_loose(o);
-    rw = (unsigned long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
+    double y[1][3], w[6];
+    double* bst = a.best + ((size_t)sc * 16 + k) * best_size(1);
+    const double* y0 = prm + DAT_P_FEQ(n) + 3 * kk;
+    const IPMOut o = nr <= NBASE ? cent_solve<W, NBASE>(a, L, g, lane, P, active, y0, y, w, bst)
+                                 : cent_solve<W, DAT_MAXROW>(a, L, g, lane, P, active, y0, y, w, bst);
     double* pf = a.pf + (size_t)sc * 3 * n;
-    if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
-      for (int k = 0; k < NB; ++k)
-        for (int c = 0; c < 3; ++c) pf[3 * k + c] = y[k][c];
-    for (int c = 0; c < 3 * n; ++c) a.fdes[(size_t)sc * 3 * n + c] = pf[c];
-    for (int k = 0; k < n; ++k) a.qstatus[(size_t)sc * n + k] = o.status;
-    a.iters[sc] = -1;
-    a.col[sc] = (unsigned char)env.collision;
-    a.mind[sc] = env.min_env_dist;
+    if (active) {
+      if (o.status == ST_OPTIMAL)  // hold the previous solution otherwise (rqp_centralized.py:441-444)
+        for (int c = 0; c < 3; ++c) pf[3 * k + c] = y[0][c];
+      for (int c = 0; c < 3; ++c) a.fdes[(size_t)sc * 3 * n + 3 * k + c] = pf[3 * k + c];
+      a.qstatus[(size_t)sc * n + k] = o.status;
+    }
+    if (k == 0) {
+      a.iters[sc] = -1;
+      a.col[sc] = (unsigned char)env.collision;
+      a.mind[sc] = env.min_env_dist;
+      q = 1;
+      ip = o.iters;
+      ib = o.inband;
+      lo = inband_loose(o);
+      rw = (unsigned long long)o.iters * (__builtin_popcount(L.sh[g].bmask) + __builtin_popcount(P.emask));
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
@@ -69,7 +138,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     ib += __shfl_xor(ib, off);
     lo += __shfl_xor(lo, off);
   }
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     atomicAdd(a.counters, q);
     atomicAdd(a.counters + 1, ip);
     atomicAdd(a.counters + 2, rw);
@@ -82,13 +151,16 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
 
 namespace dat {
 
-hipError_t launch_cent(int n, int blocks, hipStream_t stream, const KArgs& a) {
-  switch (n) {
-#define DAT_CENT_CASE(NB) \
-  case NB: hipLaunchKernelGGL(k_cent<NB>, dim3(blocks), dim3(64), 0, stream, a); break;
-    DAT_CENT_CASE(3) DAT_CENT_CASE(4) DAT_CENT_CASE(5) DAT_CENT_CASE(6)
-#undef DAT_CENT_CASE
-    default: return hipErrorInvalidValue;
+int cent_group_width(int n) { return n <= 4 ? 4 : n <= 8 ? 8 : 16; }
+
+hipError_t launch_cent(int n, int B, hipStream_t stream, const KArgs& a) {
+  if (n < 3 || n > NMAX_CENT) return hipErrorInvalidValue;
+  const int W = cent_group_width(n), G = 64 / W;
+  const int blocks = (B + G - 1) / G;
+  switch (W) {
+    case 4: hipLaunchKernelGGL(k_cent<4>, dim3(blocks), dim3(64), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL(k_cent<8>, dim3(blocks), dim3(64), 0, stream, a); break;
+    default: hipLaunchKernelGGL(k_cent<16>, dim3(blocks), dim3(64), 0, stream, a); break;
   }
   return hipGetLastError();
 }

@@ -106,11 +106,10 @@ __device__ inline void forest_of(const KArgs& a, int sc, const double** trees, i
   *nt = a.tree_off[f + 1] - a.tree_off[f];
 }
 
-// centralized control step of every scenario (dat_cent.hip): k_cent<n> for 3 <= n <= NMAX_CENT.  One
-// lane holds a whole team's QP (3n forces, 3n cones): scratch grows ~1.2 KB/lane per agent (7.2 KB at
-// n = 6), and the n = 8 instance did not complete a 4-scenario step on MI355X within 3 minutes
-// (round 3), so larger teams use the distributed controllers (C-ADMM, DD: n <= 16).
-constexpr int NMAX_CENT = 6;
-hipError_t launch_cent(int n, int blocks, hipStream_t stream, const KArgs& a);
+// centralized control step of every scenario (dat_cent.hip): k_cent<W>, one group of W = 4 / 8 / 16
+// lanes per scenario (one agent's force per lane), 3 <= n <= NMAX_CENT
+constexpr int NMAX_CENT = 16;
+int cent_group_width(int n);
+hipError_t launch_cent(int n, int B, hipStream_t stream, const KArgs& a);
 
 }  // namespace dat

@@ -643,6 +643,53 @@ inline double g_maxw;
 #define DAT_STAT_H(k) ((void)0)
 #endif
 
+// Cone-block groups.  ipm_solve sums (max, min) its per-block quantities over the blocks a lane
+// holds; a group policy extends those reductions over the W lanes of a lane group, so one QP's cone
+// blocks can live on W lanes (the centralized QP: one agent's force per lane, dat_cent.hip).  The
+// u-space algebra and the row slots are replicated on the group's lanes, so every lane must see
+// bit-identical reduced values: the reductions are xor butterflies, whose pairwise sums are computed
+// in both orders and IEEE addition / fmax / fmin are commutative.
+struct NoGrp {  // one lane holds all blocks of its QP
+  static constexpr bool on = false;
+  DAT_HD bool act() const { return true; }
+  DAT_HD int nblk(int NB) const { return NB; }
+  DAT_HD double sum(double x) const { return x; }
+  DAT_HD double max(double x) const { return x; }
+  DAT_HD double min(double x) const { return x; }
+};
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// x of the lane selected by DPP control CTRL (row-local: a group never reads another group's lanes)
+template <int CTRL>
+__device__ inline double dpp_d(double x) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(v >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+// W (4, 8 or 16) lanes, aligned to W: quad_perm xor 1, quad_perm xor 2, row_half_mirror (lane i <-> 7 - i),
+// row_mirror (i <-> 15 - i).  Each step combines the lane's partial with its partner group's.
+template <int W>
+struct GrpDpp {
+  static_assert(W == 4 || W == 8 || W == 16, "group width");
+  static constexpr bool on = true;
+  bool active;  // the lane holds a real block (phantom lanes k >= n contribute nothing)
+  int n;        // blocks of the QP
+  template <class F>
+  __device__ double red(double x, F f) const {
+    x = f(x, dpp_d<0xB1>(x));    // quad_perm [1, 0, 3, 2]
+    x = f(x, dpp_d<0x4E>(x));    // quad_perm [2, 3, 0, 1]
+    if (W >= 8) x = f(x, dpp_d<0x141>(x));   // row_half_mirror
+    if (W >= 16) x = f(x, dpp_d<0x140>(x));  // row_mirror
+    return x;
+  }
+  __device__ bool act() const { return active; }
+  __device__ int nblk(int) const { return n; }
+  __device__ double sum(double x) const { return red(active ? x : 0.0, [](double a, double b) { return a + b; }); }
+  __device__ double max(double x) const { return red(active ? x : 0.0, [](double a, double b) { return fmax(a, b); }); }
+  __device__ double min(double x) const { return red(active ? x : 1e300, [](double a, double b) { return fmin(a, b); }); }
+};
+#endif
+
 struct IPMOut {
   int status;
   int iters;
@@ -667,9 +714,10 @@ struct IPMOut {
 // row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
-template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0>
-DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
-                        double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{}) {
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP>
+DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
+                          double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
+                          bool tuned) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   // aux slot offsets (only the AUXM groups are allocated)
   constexpr int O_SC = 0;
@@ -857,6 +905,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int r = 0; r < 6; ++r) uo[r] += t[r];
     }
+    if constexpr (GRP::on) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) uo[r] = grp.sum(uo[r]);  // (MODE_CENT: no w)
+    }
   };
 
   // ---------------- initial point
@@ -866,7 +918,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   // inputs and 17-28 passes: the tuned start everywhere took C2 13 -> 20 ms and C5 81 -> 118 ms per
   // step), DD agent QPs (C3 29 -> 39 ms) and the centralized QP (also the rigid payload on the same
   // kernel, whose Jl^-1 ~ 50 grades the Newton systems)
-  const bool TUNED = MODE == MODE_CADMM && P.tuned;
+  const bool TUNED = MODE == MODE_CADMM && tuned;
   const double S0 = TUNED ? DAT_IPM_S0 : MODE == MODE_DD ? DAT_DD_S0 : 1.0;
   const double Z0 = TUNED ? DAT_IPM_Z0 : MODE == MODE_DD ? DAT_DD_Z0 : 1.0;
   const double ETA = TUNED ? DAT_IPM_ETA : MODE == MODE_DD ? DAT_DD_ETA : 0.99;
@@ -914,10 +966,14 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     double nh = 1.0 + fmax(mfz, mxf), nq = 1.0;
 #pragma unroll
     for (int l = 0; l < NR; ++l) nh = fmax(nh, 1.0 + act(l) * fabs(rb(l)));
+    {
+      double nb = 1.0;
 #pragma unroll
-    for (int k = 0; k < NB; ++k)
+      for (int k = 0; k < NB; ++k)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) nq = fmax(nq, 1.0 + fabs(P.q[k][c]));
+        for (int c = 0; c < 3; ++c) nb = fmax(nb, 1.0 + fabs(P.q[k][c]));
+      nq = fmax(nq, grp.max(nb));
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r) nq = fmax(nq, 1.0 + fabs(cup()[r]));
     NH() = nh;
@@ -928,7 +984,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
   BM() = 1e300;
   BK() = 1e300;
   out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
-  const double ideg = 1.0 / (double)(3 * NB + __builtin_popcount(mask));
+  const double ideg = 1.0 / (double)(3 * grp.nblk(NB) + __builtin_popcount(mask));
 
   DAT_PHASE_INIT(0);
   for (int it = 0;; ++it) {
@@ -955,6 +1011,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           pi[r] += cu6[r] - az[r];
         }
       }
+      // the cone blocks' parts (reduced over a lane group, GRP) before the replicated ones
+      double pobj_b = 0.0;
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         double ut[3], gz[3];
@@ -963,12 +1021,31 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           const double r = kap * y[k][c] + P.q[k][c] + ut[c] + gz[c];
-          pobj += y[k][c] * (0.5 * kap * y[k][c] + P.q[k][c]);
+          pobj_b += y[k][c] * (0.5 * kap * y[k][c] + P.q[k][c]);
           RK(k, c) = r;
           dres = fmax(dres, fabs(r));
           chk += r;
         }
       }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        double rz[9];
+        rzk_of(k, rz);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          pres = fmax(pres, fabs(rz[j]));
+          chk += rz[j];
+          gap += sk[k][j] * zk[k][j];
+        }
+      }
+      if constexpr (GRP::on) {
+        dres = grp.max(dres);
+        pres = grp.max(pres);
+        chk = grp.sum(chk);
+        gap = grp.sum(gap);
+        pobj_b = grp.sum(pobj_b);
+      }
+      pobj += pobj_b;
       {
         double Rf[6];
         if (MODE == MODE_CADMM) {
@@ -998,17 +1075,6 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           RF(r) = Rf[r];
           dres = fmax(dres, fabs(Rf[r]));
           chk += Rf[r];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        double rz[9];
-        rzk_of(k, rz);
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          pres = fmax(pres, fabs(rz[j]));
-          chk += rz[j];
-          gap += sk[k][j] * zk[k][j];
         }
       }
 #pragma unroll
@@ -1090,6 +1156,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int j = 0; j < 4; ++j) { LAM(k, 1 + j) = l1[j]; LAM(k, 5 + j) = l2[j]; }
     }
+    if constexpr (GRP::on) okc = grp.min(okc ? 1.0 : 0.0) > 0.5;
     if (!okc) {
       out.why = 3;
       break;
@@ -1134,6 +1201,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
       for (int j = 0; j < 6; ++j) DI(k, j) = Di[j];
     }
+    if constexpr (GRP::on) okc = grp.min(okc ? 1.0 : 0.0) > 0.5;
     if (!okc) {
       out.why = 4;
       break;
@@ -1220,6 +1288,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
             dinv(k, Di);
             add_UDUt(T, rt.get(k), Di, 1.0);
           }
+          if constexpr (GRP::on) {
+#pragma unroll
+            for (int k = 0; k < 21; ++k) T[k] = grp.sum(T[k]);
+          }
         }
         double Nn[21], Ln[21];
         ltl_plus_identity(Lm, T, Nn);
@@ -1277,6 +1349,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
 #pragma unroll
           for (int r = 0; r < 6; ++r) yv[r] += ut[r];
         }
+        if constexpr (GRP::on) {
+#pragma unroll
+          for (int r = 0; r < 6; ++r) yv[r] = grp.sum(yv[r]);
+        }
         if (MODE == MODE_CADMM) {
           if (has_bu) Kmul(bu, g6);
 #pragma unroll
@@ -1315,6 +1391,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           U_apply(rt.get(k), dyn[k], t);
 #pragma unroll
           for (int r = 0; r < 6; ++r) dun[r] += t[r];
+        }
+        if constexpr (GRP::on) {  // (MODE_CENT: no w)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) dun[r] = grp.sum(dun[r]);
         }
       }
 #pragma unroll
@@ -1448,6 +1528,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           for (int k = 0; k < NB; ++k)
 #pragma unroll
             for (int c = 0; c < 3; ++c) { en = fmax(en, fabs(ek[k][c])); sc = fmax(sc, fabs(RK(k, c))); }
+          if constexpr (GRP::on) {
+            en = grp.max(en);
+            sc = grp.max(sc);
+          }
 #pragma unroll
           for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(RF(r))); }
 #ifndef DAT_IPM_REF_THRESH
@@ -1504,6 +1588,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
         a = fmin(a, soc_step(l4, dss + 5));
         a = fmin(a, soc_step(l4, dzs_k[k] + 5));
       }
+      if constexpr (GRP::on) a = grp.min(a);
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
@@ -1525,6 +1610,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           const double lj = LAM(k, j);
           g += (lj + al * dss) * (lj + al * dzs_k[k][j]);
         }
+      if constexpr (GRP::on) g = grp.sum(g);
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double ds, dz;
@@ -1647,6 +1733,36 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     out.merit = BK();
   }
   return out;
+}
+
+// The reduced QP solve (ipm_attempt).  A C-ADMM agent QP on the tuned start (P.tuned: the warm closed
+// loop) that does not converge to tolerance -- diverged, hit max_iter or stalled -- is solved again from
+// the conservative start: with consensus multipliers ~1e2-1e3 (the first, cold steps of C5 / C2, a
+// stalled ADMM loop) the tuned start's small duals and 0.999 step fraction can stall (full-size C5 on the
+// CPU replica, diag/c5_cpu.py: 153 of 29.2 M agent QPs, 2 of them beyond 1e-8; every one of them
+// converges from the conservative start in 7-16 iterations).  One code instance runs both attempts
+// (unroll 1), so the retry costs no code size; out.iters counts the iterations of both.
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0,
+          class GRP = NoGrp>
+DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
+                        double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
+                        GRP grp = GRP{}) {
+  bool tuned = MODE == MODE_CADMM && P.tuned;
+  int done = 0;
+  IPMOut o;
+#pragma unroll 1
+  for (;;) {
+    // (a tuned attempt that has not converged in 20 iterations is not converging: C4's tuned solves take
+    // 4.3 on average and at most ~10)
+    o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP>(sh, er, rt, P, y0, y, w, best,
+                                                             tuned && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
+                                                             tuned);
+    o.iters += done;
+    if (!tuned || (o.why == 0 && !o.inband) || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
+    done = o.iters;
+    tuned = false;
+  }
+  return o;
 }
 
 // Solve with the smallest row-slot instantiation that covers every lane of the wavefront

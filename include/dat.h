@@ -42,7 +42,7 @@ typedef struct dat_handle dat_handle;
 typedef struct dat_config {
   int device;        /* HIP device ordinal                                               */
   int mode;          /* DAT_MODE_*                                                       */
-  int n;             /* quadrotors per payload (3 <= n <= 16; centralized n <= 6)         */
+  int n;             /* quadrotors per payload (3 <= n <= 16)                            */
   int batch;         /* number of independent scenarios B                                */
   double dt;         /* simulation step [s] (example/rqp_example.py:85: 1e-3)            */
   int hl_every;      /* simulation steps per high-level step (rqp_example.py:86: 10)     */

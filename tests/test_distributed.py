@@ -106,3 +106,23 @@ def test_bench_strong_scaling_selftest():
     assert out["scaling"] == "strong"
     assert out["config"]["scenarios_per_gpu"] == 16 and out["config"]["total_scenarios"] == 32
     assert out["stats"]["agent_qp_solves"] == 2 * 2 * 16 * 6  # ranks x steps x scenarios per rank x agents
+
+
+def test_bench_default_is_baseline_config_strong():
+    """With no --batch / --total-batch, C4 measures BASELINE configs[3] at every N: 65,536 scenarios split
+    over the ranks (strong scaling; a driver SCALE run at 8 GPUs runs 8,192 per GPU)."""
+    import sys
+
+    argv = sys.argv
+    try:
+        for extra, per, scaling_total in (([], 65536, 65536), (["--batch", "1024"], 1024, None)):
+            sys.argv = ["bench.py", "--gpus", "8"] + extra
+            a = bench.parse()
+            assert a.total_batch == scaling_total
+            B = a.batch if a.total_batch is None else bench.strong_shard(7, 8, a.total_batch)[1]
+            assert B == (8192 if scaling_total else per)
+        sys.argv = ["bench.py", "--config", "C2"]
+        a = bench.parse()
+        assert a.total_batch is None and a.batch == 1024
+    finally:
+        sys.argv = argv

@@ -230,20 +230,22 @@ def test_gpu_dd_golden():
         np.testing.assert_allclose(r.err_seq[0, : it - 1], d["tol_err"][k][: it - 1], rtol=ERR_RTOL, atol=ERR_ATOL)
 
 
-@pytest.mark.parametrize("n", [3, 4, 5, 6])
+@pytest.mark.parametrize("n", [3, 4, 5, 6, 8, 11, 16])
 def test_gpu_centralized_step_matches_oracle(n):
-    """Centralized control step (control/rqp_centralized.py:27-455, generic in n) for every team
-    size the kernel is instantiated for (k_cent<n>, dat_cent.hip): two steps (the held previous
-    solution persists), f_des within 1e-5 of the oracle's dense IPM, statuses OPTIMAL."""
+    """Centralized control step (control/rqp_centralized.py:27-455, generic in n) for team sizes on
+    every lane-group width of k_cent<W> (dat_cent.hip: W = 4 for n <= 4, 8 for n <= 8, 16 up to 16;
+    lanes n .. W-1 of a group are phantoms, B = 5 leaves most groups of the wavefront empty): two steps
+    (the held previous solution persists), f_des within 1e-5 of the oracle's dense IPM, statuses OPTIMAL."""
     from distributed_aerial_transportation_amd import scenarios
 
-    B = 4
+    B = 5
     rng = np.random.default_rng(40 + n)
     states = scenarios.perturbed_states(n, B, rng)
     acc = np.concatenate([rng.uniform(-3, 3, (B, 3)), rng.uniform(-3, 3, (B, 3))], axis=1)
     eng = _eng("centralized", n, B)
     r1 = eng.control(states, acc)
     r2 = eng.control(states, acc[::-1].copy())
+    assert eng.work()["inband_beyond_clarabel_tol"] == 0
     for b in range(B):
         ctl = oc.Centralized(osc.params(n), osc.col_radius(n))
         s = _ostate(states[b], n)
@@ -251,6 +253,33 @@ def test_gpu_centralized_step_matches_oracle(n):
         f2, _ = ctl.control(s, (acc[B - 1 - b, :3], acc[B - 1 - b, 3:]))
         assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL, (b, _rel(r1.f_des[b], f1), _rel(r2.f_des[b], f2))
         assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
+
+
+@pytest.mark.parametrize("n", [3, 6, 16])
+def test_gpu_centralized_forest_rows_match_oracle(n):
+    """Centralized QPs with binding forest CBF rows (control/rqp_centralized.py:280-337: the capsule
+    distance to every tree in range, no vision cone, alpha_env = 2): payloads 1.6-2.8 m in front of a
+    tree and moving towards it; f_des within 1e-5 of the oracle with its forest, collision flags and
+    minimum distances equal."""
+    from distributed_aerial_transportation_amd import Forest
+    from tests.test_gpu_c4 import _oforest, near_tree_states
+
+    B = 12
+    rng = np.random.default_rng(70 + n)
+    forests = [Forest.seeded(s) for s in range(4)]
+    sf = np.arange(B, dtype=np.int32) % 4
+    states = near_tree_states(n, forests, sf, rng)
+    acc = np.concatenate([rng.uniform(-1, 1, (B, 3)), np.zeros((B, 3))], axis=1)
+    eng = _eng("centralized", n, B)
+    eng.set_forests(forests, sf)
+    r = eng.control(states, acc)
+    assert eng.work()["inband_beyond_clarabel_tol"] == 0
+    for b in range(B):
+        ctl = oc.Centralized(osc.params(n), osc.col_radius(n), _oforest(forests[sf[b]]))
+        f, st = ctl.control(_ostate(states[b], n), (acc[b, :3], acc[b, 3:]))
+        assert _rel(r.f_des[b], f) < REL, (b, _rel(r.f_des[b], f))
+        assert bool(r.collision[b]) == bool(st.collision)
+        assert abs(r.min_env_dist[b] - st.min_env_dist) < 1e-6
 
 
 def test_gpu_centralized_golden():
