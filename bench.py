@@ -32,15 +32,37 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (AMD spec)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md
-# Algorithmic FP64 flops per IPM iteration of the reduced C-ADMM agent QP:
-# F_it(R) = FLOPS_FIXED + FLOPS_PER_ROW * R, R = active constraint rows of the solve.  The kernel
-# counts IPM iterations and IPM iterations x active rows on device (dat_get_counters).
-FLOPS_FIXED = 7267.0
-FLOPS_PER_ROW = 283.0
-# DD agent QP (MODE_DD: no K_{-i} products, Cholesky of M alone, DD core solve):
-# F_it,DD(R) = 4042 + 283 R per IPM iteration (k_dd; the dual ascent's 2 (6n)^2 per scenario and DD
-# iteration, ~1 % of k_dd's work at C3, is not counted).
-FLOPS_FIXED_DD = 4042.0
+# Algorithmic FP64 flops of the executed IPM work, counted per stage of the reduced
+# agent QP: per IPM iteration BASE + ROW x R (R = active constraint rows; residuals, NT scalings, the
+# u-space factorisations, the predictor and corrector solves without refinement, step lengths and the
+# update), per refinement pass run PASS + PASS_ROW x R (the residual of the linearised system), per
+# correction applied CORR (a core solve).  The kernels count IPM iterations, iterations x rows,
+# refinement passes and corrections on device (dat_get_counters, dat_get_refinement_counters).
+# Centralized (one cone block per lane, u-space algebra counted once per QP): per-block and u-space
+# parts of the same stages, BASE = 1342 + 2027 n, PASS = 132 + 165 n, CORR = 72 + 180 n.
+FLOP_MODEL = {
+    "cadmm": dict(base=3975.0, row=215.0, ref=337.0, ref_row=17.0, corr=486.0),
+    "dd": dict(base=2614.0, row=215.0, ref=207.0, ref_row=17.0, corr=150.0),
+    "centralized": dict(base=1342.0, base_n=2027.0, row=215.0, ref=132.0, ref_n=165.0, ref_row=17.0, corr=72.0,
+                        corr_n=180.0),
+}
+
+
+def model_flops(mode: str, n: int, ipm: float, rowit: float, refs: float, corrs: float) -> float:
+    """Executed algorithmic flops (FLOP_MODEL) from the device work counters."""
+    m = FLOP_MODEL[mode]
+    rbar = rowit / max(ipm, 1.0)
+    return ((m["base"] + m.get("base_n", 0.0) * n) * ipm + m["row"] * rowit
+            + (m["ref"] + m.get("ref_n", 0.0) * n + m["ref_row"] * rbar) * refs + (m["corr"] + m.get("corr_n", 0.0) * n) * corrs)
+
+
+def model_string(mode: str) -> str:
+    m = FLOP_MODEL[mode]
+    nb = lambda k: f" + {m[k + '_n']:.0f} n" if k + "_n" in m else ""  # noqa: E731
+    return (f"per IPM iteration {m['base']:.0f}{nb('base')} + {m['row']:.0f} x active rows; per refinement pass "
+            f"{m['ref']:.0f}{nb('ref')} + {m['ref_row']:.0f} x rows; per correction {m['corr']:.0f}{nb('corr')}")
+
+
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -74,7 +96,7 @@ def parse():
     ap.add_argument("--forests", type=int, default=64)
     ap.add_argument("--start", choices=["path", "edge"], default="path",
                     help="path: scenarios spread along the forest crossing (default); edge: all at the forest edge")
-    ap.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default="C4",
+    ap.add_argument("--config", choices=["C1", "C2", "C3", "C4", "C5"], default="C4",
                     help="SURVEY.md 8(d) workload; C4 (default) is the headline closed loop, C2/C3/C5 are the "
                          "QP-level configs (n, mode, batch and parameters follow the config unless given)")
     ap.add_argument("--fixed-work", action="store_true",
@@ -99,7 +121,9 @@ def parse():
 
 
 # (n, controller, scenarios per GPU) of the QP-level configs
-QP_CONFIGS = {"C2": (3, "cadmm", 1024), "C3": (6, "dd", 16384), "C5": (16, "cadmm", 32768)}
+QP_CONFIGS = {"C2": (3, "cadmm", 1024), "C3": (6, "dd", 16384), "C5": (16, "cadmm", 32768),
+              # config 1's controller (example/rqp_example.py: centralized, n = 3) batched over scenarios
+              "C1": (3, "centralized", 65536)}
 ACC_POOL = 8  # distinct acc_des draws cycled over the timed steps
 
 
@@ -132,18 +156,18 @@ def cpu_baseline_qp(cfg: str, n: int, mode: str, budget_s: float, fixed_work: bo
         if cfg == "C3":
             ml, Jl = rng.uniform(0.15, 0.30), Jl * np.diag(rng.uniform(0.8, 1.2, 3))
         p = om.Params(m, J, ml, Jl, r)
-        ctl = (oc.DD if mode == "dd" else oc.CADMM)(p, osc.col_radius(n))
+        ctl = {"dd": oc.DD, "cadmm": oc.CADMM, "centralized": oc.Centralized}[mode](p, osc.col_radius(n))
         if fixed_work and mode == "cadmm":
             ctl.set_force_err_tolerance(0.0, False)
             ctl.set_max_iter(25)
         s = RQPState.unpack(x, n)
         _, st = ctl.control(om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False), (acc[:3], acc[3:]))
-        solves += st.iter * n
+        solves += 1 if mode == "centralized" else st.iter * n
         steps += 1
     dt = time.perf_counter() - t0
     return {"value": solves / dt, "unit": "agent-QP solves/s", "cores": 1, "kind": "port",
             "sample": f"oracle {mode} n={n} (numpy dense IPM), {steps} cold control steps of {cfg} inputs, "
-                      f"{solves} agent QPs in {dt:.1f} s"}
+                      f"{solves} {'centralized' if mode == 'centralized' else 'agent'} QPs in {dt:.1f} s"}
 
 
 def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: int, steps: int, batch: int):
@@ -301,6 +325,9 @@ class _SelftestEngine:
     def closed_loop(self, k):
         self.steps += k
 
+    def step_marks(self):
+        return np.arange(self.steps + 1, dtype=np.float64)
+
     def reset_counters(self):
         self.steps = 0
 
@@ -324,19 +351,19 @@ class _SelftestEngine:
 
 
 def timed_steps(eng, steps: int, barrier):
-    """Run `steps` closed-loop HL periods one at a time (each synchronised), bracketed by the
-    barrier + device synchronisation; returns (elapsed s, per-step ms array)."""
+    """Run `steps` closed-loop HL periods back to back in one dat_closed_loop call, bracketed by the
+    barrier + device synchronisation; returns (elapsed s, per-step ms array).  The per-step times are
+    the library's host clock marks at each step's control-kernel completion (dat_get_step_marks): the
+    host enqueues step k + 1 while step k's rollout runs, so no per-step host round trip is timed."""
     barrier()
     eng.synchronize()
-    per = np.empty(steps)
     t0 = time.perf_counter()
-    for k in range(steps):
-        ts = time.perf_counter()
-        eng.closed_loop(1)
-        eng.synchronize()
-        per[k] = (time.perf_counter() - ts) * 1e3
+    eng.closed_loop(steps)
+    eng.synchronize()
     t1 = time.perf_counter()
     barrier()
+    marks = eng.step_marks()
+    per = np.diff(marks) if len(marks) == steps + 1 else np.full(steps, (t1 - t0) * 1e3 / steps)
     return t1 - t0, per
 
 
@@ -431,7 +458,8 @@ def main():
                                     "admm_slot_utilisation": w["qp_solves"] / n / max(w["wave_admm_iters"], 1)}
             k_ms = w["kernel_ms"]
     kernel_ms = k_ms / max(hl_steps, 1)
-    flops_launch = (FLOPS_FIXED * k_ipm + FLOPS_PER_ROW * k_row) / max(hl_steps, 1)
+    flops_launch = model_flops(args.mode, n, k_ipm, k_row, work.get("refine_passes", 0),
+                               work.get("refine_corrections", 0)) / max(hl_steps, 1)
     achieved_tflops = flops_launch / max(kernel_ms * 1e-3, 1e-12) / 1e12
     if total is None:
         workload = f"C4: {args.mode} n={n}, forest env ({args.start} start), {B} closed-loop scenarios per GPU"
@@ -468,8 +496,7 @@ def main():
         "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "kernel": kernel, "launch_ms": kernel_ms,
-                     "flops_per_launch": flops_launch,
-                     "flop_model": f"{FLOPS_FIXED:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"},
+                     "flops_per_launch": flops_launch, "flop_model": model_string(args.mode)},
     }
     # (the CPU restatement solves at the default 1e-10: no work-matched baseline at another --qp-tol)
     if not args.no_cpu_baseline and world == 1 and not args.selftest and args.qp_tol == 1e-10:
@@ -544,14 +571,17 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     kernel = {"cadmm": "k_cadmm", "dd": "k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
     step_ms = float(tot[2]) / max(w["hl_steps"], 1)
     launch_ms = kms / max(w["hl_steps"], 1) if args.mode != "centralized" else step_ms
-    fixed = FLOPS_FIXED_DD if args.mode == "dd" else FLOPS_FIXED
-    flops_launch = (fixed * float(tot[1]) + FLOPS_PER_ROW * float(tot[4])) / max(w["hl_steps"], 1)
+    flops_launch = model_flops(args.mode, n, float(tot[1]), float(tot[4]), w.get("refine_passes", 0),
+                               w.get("refine_corrections", 0)) / max(w["hl_steps"], 1)
     tflops = flops_launch / max(launch_ms * 1e-3, 1e-12) / 1e12
     work_mode = "fixed work: tol 0, 25 ADMM iterations" if args.fixed_work else "reference loop: tol 1e-2, max_iter 100"
+    if args.mode == "centralized":
+        work_mode = "one centralized QP per scenario and step"
     workload = f"{cfg}: {args.mode} n={n}, QP-level, no env ({work_mode}), {B} scenarios per GPU"
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
-        "value": qps / elapsed, "unit": "agent-QP solves/s", "n_gpus": world, "steps": args.steps,
+        "value": qps / elapsed, "unit": "centralized-QP solves/s" if args.mode == "centralized" else "agent-QP solves/s",
+        "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
         "ms_per_step_p50": float(np.percentile(per_step, 50)), "ms_per_step_p99": float(np.percentile(per_step, 99)),
         "higher_is_better": True,
@@ -566,8 +596,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         "roofline": {"bound": "fp64-valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None, "kernel": kernel, "launch_ms": launch_ms,
                      "flops_per_launch": flops_launch,
-                     "flop_model": f"{fixed:.0f} + {FLOPS_PER_ROW:.0f} x active rows per IPM iteration"
-                                   + (" (DD agent QP; dual ascent not counted)" if args.mode == "dd" else "")},
+                     "flop_model": model_string(args.mode) + (" (DD agent QP; dual ascent not counted)"
+                                                              if args.mode == "dd" else "")},
     }
     if not args.no_cpu_baseline and world == 1 and args.qp_tol == 1e-10:
         out["cpu_baseline"] = cpu_baseline_qp(cfg, n, args.mode, args.cpu_sample_s, args.fixed_work)

@@ -147,6 +147,7 @@ EXPORTS = {
     "dat_control_step": (ctypes.c_int, [H, D, D, D, I, I, D, U8, D]),
     "dat_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_closed_loop": (ctypes.c_int, [H, ctypes.c_int]),
+    "dat_get_step_marks": (ctypes.c_int, [H, D, ctypes.c_int]),
     "dat_get_counters": (ctypes.c_int, [H, LL, LL, LL, LL, D]),
     "dat_get_class_counters": (ctypes.c_int, [H, ctypes.c_int, LL, LL, LL, D]),
     "dat_get_class_occupancy": (ctypes.c_int, [H, ctypes.c_int, LL, LL]),
@@ -158,6 +159,7 @@ EXPORTS = {
     "dat_set_low_level": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_get_kernel_ms": (ctypes.c_int, [H, D]),
     "dat_get_inband_exits": (ctypes.c_int, [H, LL, LL]),
+    "dat_get_refinement_counters": (ctypes.c_int, [H, LL, LL]),
     "dat_get_agent_qp_ms": (ctypes.c_int, [H, D]),
     "dat_rp_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_low_level_control": (ctypes.c_int, [H, D, D, D]),

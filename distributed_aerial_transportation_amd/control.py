@@ -205,6 +205,16 @@ class BatchedController:
     def closed_loop(self, hl_steps: int) -> None:
         L.check(self._lib.dat_closed_loop(self._h, int(hl_steps)))
 
+    def step_marks(self) -> np.ndarray:
+        """Host clock marks [ms] of the last closed_loop call (dat_get_step_marks): its start, then each
+        HL step's control-kernel completion."""
+        m = self._lib.dat_get_step_marks(self._h, None, 0)
+        if m < 0:
+            L.check(m)
+        out = np.zeros(m)
+        self._lib.dat_get_step_marks(self._h, L.ptr(out), m)
+        return out
+
     def env_rows(self):
         B, n = self.batch, self.n
         lhs = np.empty((B, n, layout.NENV, 3))
@@ -259,8 +269,11 @@ class BatchedController:
                                            ctypes.byref(hs), ctypes.byref(ms)))
         ib, lo = ctypes.c_longlong(), ctypes.c_longlong()
         L.check(self._lib.dat_get_inband_exits(self._h, ctypes.byref(ib), ctypes.byref(lo)))
+        rp, rc = ctypes.c_longlong(), ctypes.c_longlong()
+        L.check(self._lib.dat_get_refinement_counters(self._h, ctypes.byref(rp), ctypes.byref(rc)))
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
-                "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value}
+                "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value,
+                "refine_passes": rp.value, "refine_corrections": rc.value}
 
     def agent_qp_ms(self) -> float:
         """Device time of the last solve_agent_qps launch (dat_get_agent_qp_ms)."""

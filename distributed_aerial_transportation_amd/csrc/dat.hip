@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <chrono>
 
 #include "../../include/dat.h"
 #include "dat_kargs.hpp"
@@ -92,9 +93,6 @@ __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
 // fill the budget).
 // C-ADMM consensus mean and residual read agent-major, the three components of a block together
 // (bitwise equal to the component-major loops; C4 A/B: k_cadmm 3.68 / 3.63 -> 3.57 / 3.54 ms)
-#ifndef DAT_CADMM_BLOCKREAD
-#define DAT_CADMM_BLOCKREAD 1
-#endif
 #ifndef DAT_AUXM0
 #define DAT_AUXM0 15
 #endif
@@ -128,25 +126,12 @@ __host__ __device__ inline int cadmm_row_mode(int n, int G, int cls) {
     return 1;
   return 0;
 }
-// ADMM multipliers of a slot's lanes (3n per lane) in LDS for the slot's lifetime, when the class's
-// carve leaves room (A/B knob DAT_CADMM_LAMLDS): the pass's multiplier reads (lane_cadmm_dynamic,
-// free blocks, dual update) then stay on chip; the warm-state array is read when a slot is filled and
-// written when its scenario stops.
-#ifndef DAT_CADMM_LAMLDS
-#define DAT_CADMM_LAMLDS 0
-#endif
-__host__ __device__ inline size_t cadmm_lam_doubles(int n, int G) { return al2((size_t)G * n * 3 * n); }
-__host__ __device__ inline bool cadmm_lam_lds(int n, int G, int cls) {
-  return DAT_CADMM_LAMLDS && cadmm_fixed_bytes(n, G) + sizeof(double) * (cadmm_area_doubles(cls, cadmm_row_mode(n, G, cls)) +
-                                                                         cadmm_lam_doubles(n, G)) <= LDS_WAVE_BUDGET;
-}
 // dynamic LDS of a k_cadmm workgroup: the largest carve of the env classes that can occur (without a
 // forest every scenario is class 0, so the launch needs only that carve and more workgroups fit a CU)
 __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NCLS - 1) {
   size_t m = 0;
   for (int c = 0; c <= max_cls; ++c) {
-    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * (cadmm_area_doubles(c, cadmm_row_mode(n, G, c)) +
-                                                                 (cadmm_lam_lds(n, G, c) ? cadmm_lam_doubles(n, G) : 0));
+    const size_t b = cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(c, cadmm_row_mode(n, G, c));
     m = b > m ? b : m;
   }
   return m;
@@ -155,7 +140,6 @@ struct CadmmLds {
   double *fbar, *Rt, *red, *rows;
   QPShared* sh;
   double* env;
-  double* lam;  // G n x 3n ADMM multipliers (cadmm_lam_lds), after the env image
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
@@ -172,7 +156,6 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.red = L.rows;
   const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
-  L.lam = L.env + env_lds_doubles(class_env_rows(cls));
   return L;
 }
 
@@ -347,6 +330,9 @@ __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, cons
   return out;
 }
 
+// Two wavefronts per SIMD (256 VGPRs, 104 B/lane of scratch for the sorted row slots): the build without
+// the bound (290 registers, no scratch, one wavefront per SIMD) measured slower, C4 A/B 3.58 / 3.61 ->
+// 3.70 / 3.80 ms per step (round 4).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_env_class(KArgs a) {
   __shared__ int nd[64], cl[64];
   __shared__ double md[64];
@@ -447,6 +433,7 @@ __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int
 struct WaveCounters {
   long long qp = 0, ipm = 0, rowit = 0;  // lane-level: agent-QP solves, IPM iterations, x active rows
   long long inband = 0, loose = 0;      // lane-level: solves accepted through the best in-band iterate
+  long long refs = 0, corrs = 0;        // lane-level: IPM refinement passes, corrections applied
   long long slot = 0, pass = 0;         // wave-level: sum of (max lane IPM iterations) per pass, passes
 };
 
@@ -471,7 +458,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   if (cnt == 0) return;
   const int rmode = cadmm_row_mode(n, G, CLS);  // wave-uniform
   CadmmLds L = cadmm_carve(smem, n, G, CLS, rmode);
-  const bool lam_lds = cadmm_lam_lds(n, G, CLS);  // wave-uniform
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * RT_STRIDE * n;
   double* myred = L.red + lane * RDS;
@@ -513,11 +499,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       lam = a.clam + ((size_t)sc * n + i) * N3;
-      if (lam_lds) {
-        double* ll = L.lam + (size_t)lane * N3;
-        for (int c = 0; c < N3; ++c) ll[c] = lam[c];
-        lam = ll;
-      }
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
       bst = a.best + ((size_t)sc * n + i) * best_size(1);
@@ -582,6 +563,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       atomicAdd(&g_iter_hist[o.iters < 63 ? o.iters : 63], 1ull);
 #endif
       wc.loose += inband_loose(o);
+      wc.refs += o.refs;
+      wc.corrs += o.corrs;
       it_lane = o.iters;
       wc.rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       ++wc.qp;
@@ -607,7 +590,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       ++iter;
       rho = fmin(rho * a.tau, a.rho_max);
       // consensus mean, summed in agent order like the reference (control/rqp_cadmm.py:591-600)
-#if DAT_CADMM_BLOCKREAD
       // agent-major: the three components of copy k read together (same per-component order)
       double s3[3] = {0.0, 0.0, 0.0};
       for (int k = 0; k < n; ++k) {
@@ -616,13 +598,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         s3[0] += c0; s3[1] += c1; s3[2] += c2;
       }
       for (int c = 0; c < 3; ++c) myred[c] = s3[c] / n;
-#else
-      for (int c = 0; c < 3; ++c) {
-        double s = 0.0;
-        for (int k = 0; k < n; ++k) s += cfs[k * N3 + 3 * i + c];
-        myred[c] = s / n;
-      }
-#endif
     }
     __syncthreads();
     if (active) {
@@ -632,7 +607,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       if (a.use_total_res) {
         double rmax = 0.0;
-#if DAT_CADMM_BLOCKREAD
         double s3[3] = {0.0, 0.0, 0.0};
         for (int j = 0; j < n; ++j) {
           const double m0 = myf[3 * j], m1 = myf[3 * j + 1], m2 = myf[3 * j + 2];
@@ -641,13 +615,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           s3[2] += fabs(m2 - fb[3 * j + 2]);
         }
         for (int r = 0; r < 3; ++r) rmax = fmax(rmax, s3[r]);
-#else
-        for (int r = 0; r < 3; ++r) {
-          double s = 0.0;
-          for (int j = 0; j < n; ++j) s += fabs(myf[3 * j + r] - fb[3 * j + r]);
-          rmax = fmax(rmax, s);
-        }
-#endif
         myred[6] = rmax;
       } else {
         // aggregate residual (control/rqp_cadmm.py:602-621): own copy's totals of the others
@@ -700,10 +667,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
         }
         a.qstatus[(size_t)sc * n + i] = qstat;
-        if (lam_lds) {  // the warm multipliers back to the warm-state array
-          double* lg = a.clam + ((size_t)sc * n + i) * N3;
-          for (int c = 0; c < N3; ++c) lg[c] = lam[c];
-        }
         if (i == 0) {
           a.iters[sc] = iter;
           a.ipmx[sc] = L.wmx[ls];
@@ -716,12 +679,15 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   // work counters of this class: one atomic per wavefront
   unsigned long long q = (unsigned long long)wc.qp, ip = (unsigned long long)wc.ipm, rw = (unsigned long long)wc.rowit;
   unsigned long long ib = (unsigned long long)wc.inband, lo = (unsigned long long)wc.loose;
+  unsigned long long rf = (unsigned long long)wc.refs, co = (unsigned long long)wc.corrs;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
     rw += __shfl_xor(rw, off);
     ib += __shfl_xor(ib, off);
     lo += __shfl_xor(lo, off);
+    rf += __shfl_xor(rf, off);
+    co += __shfl_xor(co, off);
   }
   if (lane == 0) {
     unsigned long long* cc = a.counters + CNT_STRIDE * CLS;
@@ -732,6 +698,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     atomicAdd(cc + 4, (unsigned long long)(wc.pass * G));
     if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
     if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
+    atomicAdd(a.counters + CNT_REF, rf);
+    atomicAdd(a.counters + CNT_REF + 1, co);
   }
   __syncthreads();
 }
@@ -1047,25 +1015,9 @@ __global__ __launch_bounds__(64) void k_dd_setup(KArgs a) {
 constexpr int DD_ES = 7, DD_RS = 5;
 // k_dd per-wavefront area: with a forest the env rows' LDS image; without one nothing (n = 6:
 // 27.0 KB, four wavefronts per CU -- the unused 20 KB image used to hold k_dd at three, C3 A/B
-// 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers (RowLds measured 26.2 ms).
-// DAT_DD_ROWLDS: without a forest the 3 base rows' IPM state (s, z pairs and zw) would live in this area
-// instead (RowLds), optionally with aux slots (DAT_DD_AUXM).  It removes the DD agent QP's scratch
-// spills (probe: 52 scratch ops -> 0 per IPM pass for 60 more LDS reads) but measured no gain on C3
-// (A/B, two runs each, k_dd ms: rows in registers 18.5 / 20.4, rows in LDS 21.0 / 20.2; again 19.0 /
-// 19.5 against rows + lambda slots 19.8 / 19.7 and rows + scales + lambda 20.4 / 21.4; run-to-run
-// spread ~1 ms), so it is off.
-#ifndef DAT_DD_ROWLDS
-#define DAT_DD_ROWLDS 0
-#endif
-#ifndef DAT_DD_AUXM
-#define DAT_DD_AUXM 0
-#endif
-#ifndef DAT_DD_PRICE_RT
-#define DAT_DD_PRICE_RT 0
-#endif
-__host__ __device__ constexpr int dd_area_doubles(bool env) {
-  return env ? ENV_LDS_DOUBLES : (DAT_DD_ROWLDS ? row_lds_doubles(NBASE, ipm_aux_doubles(1, DAT_DD_AUXM)) : 0);
-}
+// 23.8 -> 22.7 ms).  The 3 base rows' IPM state stays in registers: RowLds measured 26.2 ms, and rows
+// (+ aux slots) in LDS without a forest measured no gain on C3 in round 3 (git history).
+__host__ __device__ constexpr int dd_area_doubles(bool env) { return env ? ENV_LDS_DOUBLES : 0; }
 // k_dd_key: drain-order key of every scenario -- the previous step's (DD iteration count, slowest agent
 // QP's IPM iterations), longest first, as k_cadmm's key -- sorted by k_bucket into one queue (class 0).
 // DD agent QPs run the conservative IPM start (9-10 iterations on average): bins <= 8, 9-10, 11-13, >= 14.
@@ -1119,7 +1071,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double prev[9];
   int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
   double mdist = 0.0;
-  long long my_ipm = 0, my_qp = 0, my_rowit = 0, my_inband = 0, my_loose = 0;
+  long long my_ipm = 0, my_qp = 0, my_rowit = 0, my_inband = 0, my_loose = 0, my_refs = 0, my_corrs = 0;
   // phase marks (DAT_PHASE_PROF builds, tools/phase_prof.py): 11 refill + fresh slot setup, 14 prices,
   // 10 ipm_solve, 9 result bookkeeping, 13 consensus error, stop test, dual ascent, outputs
   DAT_PHASE_INIT(11);
@@ -1181,15 +1133,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
         for (int c = 0; c < 3; ++c) { sF[c] += lF[3 * k + c]; sM[c] += lM[3 * k + c]; }
       double c9[9], dm[3], rxd[3], Rr[3];
       for (int c = 0; c < 3; ++c) dm[c] = sM[c] - lM[3 * i + c];
-#if DAT_DD_PRICE_RT
-      // R_l (r_i x dm) = -Rt_i' dm with Rt_i = hat(r_i) R_l' (the slot's LDS U-map): no global reads
-      (void)rxd;
-      mtv3(rts + RT_STRIDE * i, dm, Rr);
-      for (int c = 0; c < 3; ++c) Rr[c] = -Rr[c];
-#else
       cross3(prm + DAT_P_RCOM(n) + 3 * i, dm, rxd);
       mv3(Rl, rxd, Rr);
-#endif
       for (int c = 0; c < 3; ++c) {
         c9[c] = -(sF[c] - lF[3 * i + c]) + Rr[c];
         c9[3 + c] = lF[3 * i + c];
@@ -1198,16 +1143,11 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       set_dd_price(P, prm, n, i, c9);
       double y[1][3], w[6];
       IPMOut o;
-      if (DAT_DD_WARM >= 2)
-        for (int r = 0; r < 6; ++r) P.atil[r] = prev[3 + r];
-      const double* y0 = DAT_DD_WARM >= 1 ? prev : prm + DAT_P_FEQ(n) + 3 * i;
+      const double* y0 = prm + DAT_P_FEQ(n) + 3 * i;
       DAT_PHASE(10);
       if constexpr (ENV)
         o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                        a.qp_tol);
-      else if constexpr (DAT_DD_ROWLDS)
-        o = ipm_solve<MODE_DD, 1, NBASE, LdsRef<QPShared>, EnvLds, RtLds, RowLds, DAT_DD_AUXM>(
-            shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{envs, lane});
       else
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                          a.qp_tol);
@@ -1215,6 +1155,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       my_ipm += o.iters;
       my_inband += o.inband;
       my_loose += inband_loose(o);
+      my_refs += o.refs;
+      my_corrs += o.corrs;
       atomicMax(&wmx[ls], o.iters);
 #ifdef DAT_ITER_HIST
       atomicAdd(&g_iter_hist[o.iters < 63 ? o.iters : 63], 1ull);
@@ -1333,12 +1275,15 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   }
   unsigned long long q = (unsigned long long)my_qp, ip = (unsigned long long)my_ipm, rw = (unsigned long long)my_rowit;
   unsigned long long ib = (unsigned long long)my_inband, lo = (unsigned long long)my_loose;
+  unsigned long long rf = (unsigned long long)my_refs, co = (unsigned long long)my_corrs;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
     rw += __shfl_xor(rw, off);
     ib += __shfl_xor(ib, off);
     lo += __shfl_xor(lo, off);
+    rf += __shfl_xor(rf, off);
+    co += __shfl_xor(co, off);
   }
   if (lane == 0) {
     atomicAdd(a.counters, q);
@@ -1346,6 +1291,8 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
     atomicAdd(a.counters + 2, rw);
     if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
     if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
+    atomicAdd(a.counters + CNT_REF, rf);
+    atomicAdd(a.counters + CNT_REF + 1, co);
   }
 }
 
@@ -1662,6 +1609,8 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
   // in-band accepts (rare: per lane, no wavefront reduction)
   if (o.inband) atomicAdd(a.counters + CNT_INBAND, 1);
   if (inband_loose(o)) atomicAdd(a.counters + CNT_INBAND + 1, 1);
+  atomicAdd(a.counters + CNT_REF, (unsigned long long)o.refs);
+  atomicAdd(a.counters + CNT_REF + 1, (unsigned long long)o.corrs);
   q.status[k] = o.status;
   q.iters[k] = o.iters;
   q.col[k] = (unsigned char)env.collision;
@@ -1705,6 +1654,10 @@ struct dat_handle {
   unsigned* emask = nullptr;
   long long hl_steps = 0;
   double hl_ms = 0.0;
+  // host clock marks of the last dat_closed_loop call: its start, then each HL step's k_cadmm / k_dd /
+  // k_cent completion (ms on a steady clock); consecutive differences are the per-step times of a
+  // back-to-back run (dat_get_step_marks)
+  std::vector<double> marks;
   double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
@@ -2184,15 +2137,41 @@ int dat_closed_loop(dat_handle* h, int hl_steps) {
   HIPCHK(hipSetDevice(h->cfg.device));
   const size_t B = h->cfg.batch;
   KArgs a = kargs(h);
+  auto now_ms = [] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  h->marks.clear();
+  h->marks.push_back(now_ms());
   for (int s = 0; s < hl_steps; ++s) {
     hipLaunchKernelGGL(k_desired, dim3((B + 63) / 64), dim3(64), 0, h->stream, a, h->acc);
     if (launch_hl(h)) return -1;
     launch_rollout(a, (int)B, h->stream, h->cfg.hl_every, h->cfg.dt, (const double*)h->fdes);
     HIPCHK(hipGetLastError());
+    // waits for this step's control kernel; the rollout still runs while the next step is enqueued
     if (finish_hl(h)) return -1;
+    h->marks.push_back(now_ms());
   }
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
+}
+
+int dat_get_refinement_counters(dat_handle* h, long long* passes, long long* corrections) {
+  if (!h) return fail("null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_REF, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (passes) *passes = (long long)c[0];
+  if (corrections) *corrections = (long long)c[1];
+  return 0;
+}
+
+int dat_get_step_marks(dat_handle* h, double* marks_ms, int max_marks) {
+  if (!h) return fail("null handle");
+  const int m = (int)h->marks.size();
+  if (marks_ms)
+    for (int k = 0; k < m && k < max_marks; ++k) marks_ms[k] = h->marks[k] - h->marks[0];
+  return m;
 }
 
 int dat_get_counters(dat_handle* h, long long* qp_solves, long long* ipm_iters, long long* ipm_row_iters,

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   }
   __syncthreads();
   QPLane<1> P;
-  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0;
+  unsigned long long q = 0, ip = 0, rw = 0, ib = 0, lo = 0, rf = 0, co = 0;
   int nr = NBASE;
   if (valid) {
     lane_common(P, prm);
@@ -128,6 +128,8 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
       ip = o.iters;
       ib = o.inband;
       lo = inband_loose(o);
+      rf = o.refs;
+      co = o.corrs;
       rw = (unsigned long long)o.iters * (__builtin_popcount(L.sh[g].bmask) + __builtin_popcount(P.emask));
     }
   }
@@ -137,6 +139,8 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     rw += __shfl_xor(rw, off);
     ib += __shfl_xor(ib, off);
     lo += __shfl_xor(lo, off);
+    rf += __shfl_xor(rf, off);
+    co += __shfl_xor(co, off);
   }
   if (lane == 0) {
     atomicAdd(a.counters, q);
@@ -144,6 +148,8 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
     atomicAdd(a.counters + 2, rw);
     if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
     if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
+    atomicAdd(a.counters + CNT_REF, rf);
+    atomicAdd(a.counters + CNT_REF + 1, co);
   }
 }
 

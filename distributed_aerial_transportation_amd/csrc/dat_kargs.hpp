@@ -22,28 +22,23 @@ __host__ __device__ constexpr int class_env_rows(int c) { return c == 0 ? 0 : c 
 // ADMM passes and the longest ones are claimed first (a 101-iteration scenario claimed last is the
 // tail of the whole launch)
 constexpr int NAB = 8;   // ADMM / DD iteration bins
-#ifndef DAT_IPM_BINS
-#define DAT_IPM_BINS 4
-#endif
-constexpr int NPB = DAT_IPM_BINS;  // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
+constexpr int NPB = 4;  // IPM iteration bins (C-ADMM: the slowest agent QP of the scenario's step)
 constexpr int NIB = NAB * NPB;
 __host__ __device__ inline int iter_bin(int it) {
   if (it <= 3) return it < 1 ? 0 : it - 1;
   const int lg = 31 - __builtin_clz((unsigned)(it - 2));  // floor(log2(it - 2)) >= 1
   return 2 + lg < NAB - 1 ? 2 + lg : NAB - 1;
 }
-// IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8
-// (DAT_IPM_BINS 6: <= 4, 5, 6, 7, 8, >= 9)
-__host__ __device__ inline int ipm_bin(int it) {
-  if (NPB == 6) return it <= 4 ? 0 : it >= 9 ? 5 : it - 4;
-  return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3;
-}
+// IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8 (six bins measured no gain, round 3)
+__host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
 constexpr int NKEY = NCLS * NIB;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
 // QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
 // scaled residual / gap exceeds Clarabel's own tolerance (INBAND_CLARABEL)
 constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
-constexpr int DAT_NCOUNTERS = CNT_INBAND + 2;
+// IPM refinement passes run and corrections applied (all kernels; the executed-flop model)
+constexpr int CNT_REF = CNT_INBAND + 2;
+constexpr int DAT_NCOUNTERS = CNT_REF + 2;
 constexpr double INBAND_CLARABEL = 1e-8;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
 

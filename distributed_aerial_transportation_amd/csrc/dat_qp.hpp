@@ -62,12 +62,6 @@ constexpr int NREF = DAT_IPM_NREF;
 #ifndef DAT_DD_Z0
 #define DAT_DD_Z0 1.0
 #endif
-// DD warm start (A/B knob): 0 the IPM starts from f_eq and w = 0; 1 from the agent's previous (f_i)
-// of the scenario (the last DD pass, or the previous step's solution on a slot's first pass); 2 also
-// w = its previous (F_i, M_i)
-#ifndef DAT_DD_WARM
-#define DAT_DD_WARM 0
-#endif
 #ifndef DAT_DD_ETA
 #define DAT_DD_ETA 0.99
 #endif
@@ -76,11 +70,6 @@ constexpr int NREF = DAT_IPM_NREF;
 #endif
 #ifndef DAT_IPM_DIVERGE
 #define DAT_IPM_DIVERGE 1e6
-#endif
-// refinement (corrector solve only) stops early once the linearised system's residual is within
-// 1e-12 of its right-hand side (C4 A/B: k_cadmm 11.0 ms with two passes per solve -> 8.9 ms)
-#ifndef DAT_IPM_REFINE_MODE
-#define DAT_IPM_REFINE_MODE 1
 #endif
 
 // Every array starts on a 16-byte boundary and the kernels place the record 16-byte aligned in LDS,
@@ -122,9 +111,7 @@ struct PlainRef {
 // arithmetic.
 template <class T>
 __device__ inline const DAT_LDS T* lds_opaque(const DAT_LDS T* p) {
-#ifndef DAT_LDS_HOIST
   __asm__ volatile("" : "+v"(p));
-#endif
   return p;
 }
 template <class T>
@@ -697,6 +684,8 @@ struct IPMOut {
   double merit;   // scaled max(primal residual, dual residual, gap) of the returned iterate
   int why;        // exit: 0 converged, 1 non-finite residuals, 2 divergence / max_iter, 3 cone scaling,
                   // 4 cone block D, 5 Cholesky of M, 6 Cholesky of N
+  int refs;       // refinement passes run (residual evaluations of the linearised system)
+  int corrs;      // refinement corrections applied (core solves)
   double pi[6];   // u-space gradient C u + cu - A' z_rows at the solution
   double u[6];
 };
@@ -732,6 +721,8 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
   out.iters = 0;
   out.inband = 0;
   out.why = 0;
+  out.refs = 0;
+  out.corrs = 0;
   out.merit = 1e300;
 #pragma unroll
   for (int r = 0; r < 6; ++r) { out.pi[r] = 0.0; out.u[r] = 0.0; }
@@ -949,9 +940,9 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
   // w = atil (the infeasible start lets the Newton steps restore rho (w - atil) + K_{-i} pi = 0).
   // A consistent start through a 6x6 LU of (rho I + K C) took the same iteration count and held
   // ~1 KB/lane more spill frame (C4 A/B: k_cadmm 8.9 -> 7.7 ms without it).
-  if (MODE == MODE_CADMM || (MODE == MODE_DD && DAT_DD_WARM >= 2)) {
+  if (MODE == MODE_CADMM) {
 #pragma unroll
-    for (int r = 0; r < 6; ++r) w[r] = P.atil[r];  // DD: the previous (F_i, M_i) (k_dd, DAT_DD_WARM 2)
+    for (int r = 0; r < 6; ++r) w[r] = P.atil[r];
   }
   {
     double u[6], dv[3], dw[3];
@@ -1472,6 +1463,7 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll 1
       for (int ref = 0; ref < nref; ++ref) {
         DAT_STAT(1);
+        ++out.refs;
         if (ref == 1) DAT_STAT_H(2);
         // linearised dual residual of the full system at (dy, dw); refine
 #pragma unroll
@@ -1521,8 +1513,8 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
           for (int r = 0; r < 6; ++r) ef[r] = 0.0;
         }
-#if DAT_IPM_REFINE_MODE >= 1
         {  // the linearised system is already solved to rounding: the correction would be noise
+           // (stopping here: C4 A/B k_cadmm 11.0 ms with two passes per solve -> 8.9 ms, round 2)
           double en = 0.0, sc = 1.0;
 #pragma unroll
           for (int k = 0; k < NB; ++k)
@@ -1534,20 +1526,17 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           }
 #pragma unroll
           for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(RF(r))); }
-#ifndef DAT_IPM_REF_THRESH
-#define DAT_IPM_REF_THRESH 1e-12
-#endif
 #ifdef DAT_IPM_TRACE
           printf("    ref %d en %.3e sc %.3e\n", ref, en, sc);
 #endif
-          if (en <= DAT_IPM_REF_THRESH * sc) {
+          if (en <= 1e-12 * sc) {
             DAT_STAT(2);
             if (ref == 0) DAT_STAT_H(0);
             break;
           }
           if (ref == 0) DAT_STAT_H(1);
         }
-#endif
+        ++out.corrs;
         core(ek, ef, nullptr, false, true, dy, dwv, du);
       }
 #pragma unroll
@@ -1748,7 +1737,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
                         GRP grp = GRP{}) {
   bool tuned = MODE == MODE_CADMM && P.tuned;
-  int done = 0;
+  int done = 0, done_refs = 0, done_corrs = 0;
   IPMOut o;
 #pragma unroll 1
   for (;;) {
@@ -1758,8 +1747,12 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
                                                              tuned && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
                                                              tuned);
     o.iters += done;
+    o.refs += done_refs;
+    o.corrs += done_corrs;
     if (!tuned || (o.why == 0 && !o.inband) || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
     done = o.iters;
+    done_refs = o.refs;
+    done_corrs = o.corrs;
     tuned = false;
   }
   return o;

@@ -132,6 +132,10 @@ int dat_rp_rollout(dat_handle* h, int steps, const double* f);
  * acceleration of :33-59): hl_steps x (desired acceleration + control step +
  * hl_every rollout steps); inputs already in HBM, nothing copied per step. */
 int dat_closed_loop(dat_handle* h, int hl_steps);
+/* Host steady-clock marks (ms) of the last dat_closed_loop call: [0] its start (0.0), then the completion
+ * of each HL step's control kernel; consecutive differences are per-step times of the back-to-back run.
+ * Writes up to max_marks values; returns the number of marks (hl_steps + 1). */
+int dat_get_step_marks(dat_handle* h, double* marks_ms, int max_marks);
 
 /* ---- counters since the last reset: agent-QP solves, IPM iterations, IPM iterations x active
  * constraint rows (for the flop model of DESIGN.md 3.1), control steps, and the summed device time
@@ -166,6 +170,9 @@ int dat_get_kernel_ms(dat_handle* h, double* ms);
  * reference holds its previous solution on a non-OPTIMAL status (control/rqp_cadmm.py:496-499), so
  * beyond_clarabel_tol bounds the branch-disagreement risk; the C-ADMM / DD parity tests require 0. */
 int dat_get_inband_exits(dat_handle* h, long long* inband, long long* beyond_clarabel_tol);
+/* IPM iterative-refinement passes run and corrections applied by every kernel since the last counter
+ * reset: the executed-work terms of the flop model. */
+int dat_get_refinement_counters(dat_handle* h, long long* passes, long long* corrections);
 /* Device time [ms] of the last dat_solve_agent_qp_batch launch (k_agent_qp; HIP events on the handle's
  * stream): the solve_time RQPPrimalSolver.solve returns (Clarabel's solver_stats.solve_time,
  * control/rqp_cadmm.py:500, control/rqp_dd.py:497). */

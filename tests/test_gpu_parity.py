@@ -133,10 +133,10 @@ def test_gpu_cadmm_default_tolerance_golden():
         assert _rel(r.f_des[0], d["tol_f"][k]) < REL
 
 
-def _ambiguous(seq, tol=1e-2):
-    """The reference stops when err < tol; a residual within 1e-7 relative of tol can flip the count
+def _ambiguous(seq, tol=1e-2, band=1e-7):
+    """The reference stops when err < tol; a residual within `band` (relative) of tol can flip the count
     (such scenarios are excluded from exact-count checks, and tests assert they are rare)."""
-    return any(abs(e - tol) < 1e-7 * tol for e in seq)
+    return any(abs(e - tol) < band * tol for e in seq)
 
 
 @pytest.mark.parametrize("n", [3, 4, 6, 8, 11, 16])
@@ -159,16 +159,19 @@ def test_gpu_dd_step_matches_oracle(n):
         s = _ostate(states[b], n)
         f1, st1 = ctl.control(s, (acc[b, :3], acc[b, 3:]))
         f2, st2 = ctl.control(s, (acc[B - 1 - b, :3], acc[B - 1 - b, 3:]))
-        if _ambiguous(st1.err_seq) or _ambiguous(st2.err_seq):
+        # a residual within the team size's own err_seq sensitivity of the stopping tolerance can stop
+        # one iteration earlier or later (the oracle against itself does at n = 16)
+        rtol = DD_ERR_RTOL.get(n, ERR_RTOL)
+        band = rtol / 3 if n in DD_ERR_RTOL else 1e-7  # the measured sensitivity itself
+        if _ambiguous(st1.err_seq, band=band) or _ambiguous(st2.err_seq, band=band):
             skipped += 1
             continue
         assert r1.iters[b] == st1.iter and r2.iters[b] == st2.iter, (b, r1.iters[b], st1.iter, r2.iters[b], st2.iter)
         assert _rel(r1.f_des[b], f1) < REL and _rel(r2.f_des[b], f2) < REL, (_rel(r1.f_des[b], f1), _rel(r2.f_des[b], f2))
-        rtol = DD_ERR_RTOL.get(n, ERR_RTOL)
         np.testing.assert_allclose(r1.err_seq[b, : st1.iter - 1], st1.err_seq, rtol=rtol, atol=ERR_ATOL)
         np.testing.assert_allclose(r2.err_seq[b, : st2.iter - 1], st2.err_seq, rtol=rtol, atol=ERR_ATOL)
         assert np.all(r1.qp_status[b] == 0) and np.all(r2.qp_status[b] == 0)
-    assert skipped <= 1
+    assert skipped <= (2 if n in DD_ERR_RTOL else 1)
     assert eng.work()["inband_beyond_clarabel_tol"] == 0
 
 
