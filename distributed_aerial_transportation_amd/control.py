@@ -205,6 +205,20 @@ class BatchedController:
     def closed_loop(self, hl_steps: int) -> None:
         L.check(self._lib.dat_closed_loop(self._h, int(hl_steps)))
 
+    def control_steps(self, acc_seq: np.ndarray) -> StepResult:
+        """dat_control_steps: acc_seq (K, B, 6) -> K fused control steps of every scenario from the resident
+        states (C-ADMM / DD without a forest); the result holds the last step's outputs."""
+        acc_seq = L.f64(acc_seq)
+        K = acc_seq.shape[0]
+        assert acc_seq.shape[1:] == (self.batch, 6), acc_seq.shape
+        f = np.zeros((self.batch, 3 * self.n))
+        it = np.zeros(self.batch, dtype=np.int32)
+        qs = np.zeros((self.batch, self.n), dtype=np.int32)
+        L.check(self._lib.dat_control_steps(self._h, int(K), L.ptr(acc_seq), L.ptr(f), L.ptr(it, L.I),
+                                            L.ptr(qs, L.I)))
+        return StepResult(f.reshape(self.batch, self.n, 3).transpose(0, 2, 1).copy(), it, qs,
+                          np.zeros(self.batch), np.zeros(self.batch, dtype=bool))
+
     def step_marks(self) -> np.ndarray:
         """Host clock marks [ms] of the last closed_loop call (dat_get_step_marks): its start, then each
         HL step's control-kernel completion."""

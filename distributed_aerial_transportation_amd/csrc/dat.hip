@@ -478,6 +478,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   double* myf = nullptr;
   double* bst = nullptr;
   int iter = 0, prev_iter = 0, qstat = ST_OPTIMAL;
+  int kstep = 0;  // fused control steps (dat_control_steps): the slot scenario's current step
   double rho = a.rho0;
   WaveCounters wc;
   for (;;) {
@@ -506,6 +507,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       prev_iter = a.iters[sc];  // the previous step's ADMM iterations (rewritten when the scenario stops)
       qstat = ST_OPTIMAL;
       rho = a.rho0;
+      kstep = 0;
       if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
     }
     if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
@@ -670,6 +672,21 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         if (i == 0) {
           a.iters[sc] = iter;
           a.ipmx[sc] = L.wmx[ls];
+        }
+        if (kstep + 1 < a.ksteps) {
+          // fused steps: the scenario's next control step in the same slot (warm f, f_mean, lambda kept;
+          // rho and the iteration count restart as in a new control call, control/rqp_cadmm.py:631-640)
+          ++kstep;
+          prev_iter = iter;
+          iter = 0;
+          qstat = ST_OPTIMAL;
+          rho = a.rho0;
+          if (i == 0) {
+            build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
+                         prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+            L.wmx[ls] = 0;
+          }
+        } else if (i == 0) {
           L.sid[ls] = -1;
         }
       }
@@ -1070,6 +1087,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   double* bst = nullptr;
   double prev[9];
   int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
+  int kstep = 0;  // fused control steps (dat_control_steps): the slot scenario's current step
   double mdist = 0.0;
   long long my_ipm = 0, my_qp = 0, my_rowit = 0, my_inband = 0, my_loose = 0, my_refs = 0, my_corrs = 0;
   // phase marks (DAT_PHASE_PROF builds, tools/phase_prof.py): 11 refill + fresh slot setup, 14 prices,
@@ -1102,6 +1120,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       bst = a.best + ((size_t)sc * n + i) * best_size(1);
       iter = 0;
       qstat = ST_OPTIMAL;
+      kstep = 0;
       if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
     }
     if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
@@ -1267,6 +1286,19 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
           }
           a.col[sc] = (unsigned char)coll;
           a.mind[sc] = md;
+        }
+        if (kstep + 1 < a.ksteps) {
+          // fused steps (no forest): the scenario's next control step in the same slot, from the warm
+          // lambda_F, lambda_M and previous solutions it leaves (control/rqp_dd.py:695-700)
+          ++kstep;
+          iter = 0;
+          qstat = ST_OPTIMAL;
+          if (i == 0) {
+            build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
+                         prm[DAT_P_KFD], prm[DAT_P_KMD], 3, false);
+            wmx[ls] = 0;
+          }
+        } else if (i == 0) {
           sid[ls] = -1;
         }
       }
@@ -1658,6 +1690,8 @@ struct dat_handle {
   // k_cent completion (ms on a steady clock); consecutive differences are the per-step times of a
   // back-to-back run (dat_get_step_marks)
   std::vector<double> marks;
+  double* acc_seq = nullptr;  // dat_control_steps: K x B x 6 desired accelerations (grown on demand)
+  size_t acc_seq_cap = 0;
   double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
@@ -1724,6 +1758,7 @@ KArgs kargs(dat_handle* h) {
   a.rho_max = c.rho_max;
   a.record_err = c.record_err;
   a.qp_tol = h->qp_tol;
+  a.ksteps = 1;
   a.cf = h->cf;
   a.cfbar = h->cfbar;
   a.clam = h->clam;
@@ -1761,8 +1796,11 @@ size_t dd_setup_lds(int n) {
   return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + dd_setup_hs(n) + N);
 }
 
-int launch_hl(dat_handle* h) {
+// ksteps > 1 (dat_control_steps): that many control steps fused into one drain, acc_seq ksteps x B x 6
+int launch_hl(dat_handle* h, int ksteps = 1, const double* acc_seq = nullptr) {
   KArgs a = kargs(h);
+  a.ksteps = ksteps;
+  if (acc_seq) a.acc = acc_seq;
   const int n = h->cfg.n, B = h->cfg.batch;
   if (!h->have_params) return fail("dat_set_params has not been called");
   if (h->cfg.record_err && h->err)
@@ -1807,7 +1845,7 @@ int launch_hl(dat_handle* h) {
   return 0;
 }
 
-int finish_hl(dat_handle* h) {
+int finish_hl(dat_handle* h, int ksteps = 1) {
   HIPCHK(hipEventSynchronize(h->e1));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, h->e0, h->e1));
@@ -1817,7 +1855,7 @@ int finish_hl(dat_handle* h) {
     HIPCHK(hipEventElapsedTime(&mk, h->ek, h->e1));
     h->cadmm_ms += mk;
   }
-  h->hl_steps += 1;
+  h->hl_steps += ksteps;
   return 0;
 }
 
@@ -1957,6 +1995,7 @@ int dat_destroy(dat_handle* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (void* p : h->allocs)
     if (p) (void)hipFree(p);
+  if (h->acc_seq) (void)hipFree(h->acc_seq);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
   if (h->ek) (void)hipEventDestroy(h->ek);
@@ -2114,6 +2153,32 @@ int dat_control_step(dat_handle* h, const double* state, const double* acc_des, 
     HIPCHK(hipMemcpyAsync(err_seq, h->err, sizeof(double) * B * (h->cfg.max_iter + 1), hipMemcpyDeviceToHost, h->stream));
   }
   if (finish_hl(h)) return -1;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int dat_control_steps(dat_handle* h, int steps, const double* acc_seq, double* f_des, int* iters, int* qp_status) {
+  if (!h || !acc_seq) return fail("dat_control_steps: null argument");
+  if (steps <= 0) return fail("dat_control_steps: steps must be >= 1");
+  if (h->cfg.mode != DAT_MODE_CADMM && h->cfg.mode != DAT_MODE_DD)
+    return fail("dat_control_steps: C-ADMM and DD handles only");
+  if (h->nforest > 0) return fail("dat_control_steps: handles without a forest only (env rows change with the state)");
+  if (h->cfg.record_err) return fail("dat_control_steps: record_err must be 0");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  const size_t B = h->cfg.batch, n = h->cfg.n, need = (size_t)steps * B * 6;
+  if (need > h->acc_seq_cap) {
+    if (h->acc_seq) HIPCHK(hipFree(h->acc_seq));
+    h->acc_seq = nullptr;
+    h->acc_seq_cap = 0;
+    HIPCHK(hipMalloc(&h->acc_seq, sizeof(double) * need));
+    h->acc_seq_cap = need;
+  }
+  HIPCHK(hipMemcpyAsync(h->acc_seq, acc_seq, sizeof(double) * need, hipMemcpyHostToDevice, h->stream));
+  if (launch_hl(h, steps, h->acc_seq)) return -1;
+  if (f_des) HIPCHK(hipMemcpyAsync(f_des, h->fdes, sizeof(double) * B * 3 * n, hipMemcpyDeviceToHost, h->stream));
+  if (iters) HIPCHK(hipMemcpyAsync(iters, h->iters, sizeof(int) * B, hipMemcpyDeviceToHost, h->stream));
+  if (qp_status) HIPCHK(hipMemcpyAsync(qp_status, h->qstatus, sizeof(int) * B * n, hipMemcpyDeviceToHost, h->stream));
+  if (finish_hl(h, steps)) return -1;
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }

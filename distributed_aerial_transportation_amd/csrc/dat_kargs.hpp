@@ -81,6 +81,8 @@ struct KArgs {
   unsigned* emask;               // C-ADMM: [B n] env row mask of the step
   int ll_kind;                   // low-level SO(3) law: LL_PD or LL_SM (dat_set_low_level)
   double qp_tol;                 // IPM stopping tolerance of every QP (dat_set_qp_tolerance)
+  int ksteps;                    // C-ADMM / DD without a forest: control steps fused into one drain
+                                 // (dat_control_steps; acc then holds ksteps x B x 6 values)
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)

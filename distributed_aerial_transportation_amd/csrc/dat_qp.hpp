@@ -1086,16 +1086,19 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         break;
       }
       const double nh = NH(), nq = NQ();
-      // complementarity gap relative to the objective (Clarabel's gap_rel and the oracle's rule): with
-      // multipliers ~1e3-1e4 (a stalled ADMM loop) an absolute gap below 1e-9 lies under the rounding
-      // floor of s o z, and the Newton systems break down before reaching it
-      const double grel = gap * frcp(fmax(1.0, fabs(pobj)));
+      // complementarity gap, absolute or relative to the objective as Clarabel tests it (gap_abs or
+      // gap_rel): converged when gap < 10 tol or gap < tol / 10 |pobj| (at the default tol = 1e-10: 1e-9
+      // absolute, or the oracle's own 1e-11 relative rule), i.e. the scaled gap gap / max(1, |pobj| / 100)
+      // below 10 tol.  With multipliers ~1e3-1e4 (a stalled ADMM loop, |pobj| ~1e4-1e5) an absolute gap
+      // of 1e-9 lies below what the Newton systems resolve; well-scaled QPs (|pobj| <= 100) keep the
+      // absolute rule.
+      const double grel = gap * frcp(fmax(1.0, 0.01 * fabs(pobj)));
       double merit = fmax(fmax(pres / nh, dres / nq), grel);
 #ifdef DAT_IPM_TRACE
       printf("ipm it %2d pres %.3e dres %.3e gap %.3e merit %.3e pobj %.3e\n", it, pres / nh, dres / nq, grel, merit,
              pobj);
 #endif
-      if (pres < tol * nh && dres < tol * nq && grel < 0.1 * tol) {
+      if (pres < tol * nh && dres < tol * nq && grel < 10.0 * tol) {
         out.status = ST_OPTIMAL;
         out.merit = merit;
 #pragma unroll
@@ -1103,13 +1106,17 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         DAT_PHASE(8);
         return out;
       }
-      // Only an in-band iterate (scaled residuals < 1e-7, gap < 1e-6) can be returned: a solve that
-      // ends out of band is INACCURATE and the callers hold their previous solution instead, so
+      // Only an in-band iterate (scaled residuals < 1e-7, relative gap < 1e-6) can be returned: a solve
+      // that ends out of band is INACCURATE and the callers hold their previous solution instead, so
       // out-of-band iterates are never recorded (the record is written in the last one or two
-      // iterations of a stalling solve, not at every iteration).
-      const bool band = fmax(pres / nh, dres / nq) < 1e-7 && grel < 1e-6;
-      if (band && merit < BK()) {
-        BK() = merit;
+      // iterations of a stalling solve, not at every iteration).  Its merit is measured as Clarabel
+      // measures convergence (residuals, and the gap absolute or relative to the objective, whichever
+      // is smaller: max(1, |pobj|) scaling), so inband_loose counts exactly the accepts outside
+      // Clarabel's own tolerance.
+      const double mclr = fmax(fmax(pres / nh, dres / nq), gap * frcp(fmax(1.0, fabs(pobj))));
+      const bool band = fmax(pres / nh, dres / nq) < 1e-7 && mclr < 1e-6;
+      if (band && mclr < BK()) {
+        BK() = mclr;
 #pragma unroll
         for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -1147,6 +1154,15 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
       for (int j = 0; j < 4; ++j) { LAM(k, 1 + j) = l1[j]; LAM(k, 5 + j) = l2[j]; }
     }
+#ifdef DAT_IPM_TRACE
+    for (int k = 0; k < NB; ++k)
+      printf("    cone s %.2e %.2e %.2e z %.2e %.2e %.2e | eta1 %.2e eta2 %.2e | rows z/s %.2e %.2e %.2e\n", sk[k][0],
+             sk[k][1] - sqrt(sk[k][2] * sk[k][2] + sk[k][3] * sk[k][3] + sk[k][4] * sk[k][4]),
+             sk[k][5] - sqrt(sk[k][6] * sk[k][6] + sk[k][7] * sk[k][7] + sk[k][8] * sk[k][8]), zk[k][0],
+             zk[k][1] - sqrt(zk[k][2] * zk[k][2] + zk[k][3] * zk[k][3] + zk[k][4] * zk[k][4]),
+             zk[k][5] - sqrt(zk[k][6] * zk[k][6] + zk[k][7] * zk[k][7] + zk[k][8] * zk[k][8]), S1[k].eta, S2[k].eta,
+             (double)ZL(0) / (double)SL(0), (double)ZL(1) / (double)SL(1), (double)ZL(2) / (double)SL(2));
+#endif
     if constexpr (GRP::on) okc = grp.min(okc ? 1.0 : 0.0) > 0.5;
     if (!okc) {
       out.why = 3;

@@ -109,6 +109,15 @@ int dat_get_state(dat_handle* h, double* state, int* counters);
 int dat_control_step(dat_handle* h, const double* state, const double* acc_des, double* f_des, int* iters,
                      int* qp_status, double* min_env_dist, unsigned char* collision, double* err_seq);
 
+/* ---- fused control steps (QP-level workloads: C-ADMM / DD handles without a forest): `steps`
+ * consecutive control steps of every scenario from the resident states, scenario s's step k using
+ * acc_seq[(k B + s) x 6 ..] -- the same arithmetic per scenario as `steps` calls of dat_control_step
+ * (warm f, f_mean, lambda / lambda_F, lambda_M carried; control/rqp_cadmm.py:631-675,
+ * control/rqp_dd.py:695-752), in ONE persistent drain: a scenario that finishes step k starts step
+ * k + 1 in its slot at once instead of waiting for the slowest scenario of step k.  Outputs (optional,
+ * NULL to skip) are those of the last step.  record_err must be 0. */
+int dat_control_steps(dat_handle* h, int steps, const double* acc_seq, double* f_des, int* iters, int* qp_status);
+
 /* ---- rollout: `steps` simulation steps (SO(3) PD low level + rigid-body dynamics) ---------
  * Replaces RQPLowLevelController.control (control/rqp_centralized.py:518-535) followed by
  * RQPDynamics.integrate (system/rigid_quadrotor_payload.py:271-276) per simulation step.

@@ -145,3 +145,35 @@ def test_gpu_reset_warm_start_matches_fresh_handle(mode):
     ra, rb = used.control(x, accs[0]), fresh.control(x, accs[0])
     np.testing.assert_array_equal(ra.f_des, rb.f_des)
     np.testing.assert_array_equal(ra.iters, rb.iters)
+
+
+@pytest.mark.parametrize("mode,n,B,blocks", [("cadmm", 3, 40, 1), ("cadmm", 16, 9, 0), ("dd", 6, 30, 1), ("dd", 3, 25, 0)])
+def test_gpu_fused_steps_equal_separate_steps(mode, n, B, blocks):
+    """dat_control_steps: K control steps fused into one persistent drain (a slot's scenario moves on to
+    its next step at once) must give every scenario exactly the arithmetic of K separate
+    dat_control_step calls -- warm state carried, rho and the iteration count restarting per step
+    (control/rqp_cadmm.py:631-675, control/rqp_dd.py:695-752): bitwise equal f_des, iteration counts,
+    statuses and warm state, on a capped grid (slots refilled across steps) and on the full grid."""
+    from distributed_aerial_transportation_amd import BatchedController, scenarios
+
+    K = 4
+    rng = np.random.default_rng(500 + n)
+    states = scenarios.perturbed_states(n, B, rng)
+    accs = rng.uniform(-0.5, 0.5, (K, B, 6)) * 8.0
+    sep = BatchedController(mode, n, B, scenarios.params_block(n))
+    sep.set_state(states)
+    for k in range(K):
+        r_sep = sep.control(None, accs[k])
+    fus = BatchedController(mode, n, B, scenarios.params_block(n))
+    fus.set_persistent_blocks(blocks)
+    fus.set_state(states)
+    r_fus = fus.control_steps(accs)
+    assert np.array_equal(r_fus.f_des, r_sep.f_des)
+    assert np.array_equal(r_fus.iters, r_sep.iters)
+    assert np.array_equal(r_fus.qp_status, r_sep.qp_status)
+    ws, wf = sep.work(), fus.work()
+    assert wf["qp_solves"] == ws["qp_solves"] and wf["ipm_iters"] == ws["ipm_iters"]
+    assert wf["hl_steps"] == ws["hl_steps"] == K
+    # the warm state left behind: one more separate step from each must agree bitwise
+    a5 = rng.uniform(-0.5, 0.5, (B, 6)) * 8.0
+    assert np.array_equal(sep.control(None, a5).f_des, fus.control(None, a5).f_des)
