@@ -101,6 +101,9 @@ def parse():
                          "QP-level configs (n, mode, batch and parameters follow the config unless given)")
     ap.add_argument("--fixed-work", action="store_true",
                     help="C2/C5 mode (ii): tol 0, 25 ADMM iterations (test/control/test_rqpcontrollers.py:106-110)")
+    ap.add_argument("--fused", action="store_true",
+                    help="C2/C3/C5: the timed steps as ONE dat_control_steps call (each scenario starts its next "
+                         "control step as soon as its previous one ends; ms_per_step = elapsed / steps)")
     ap.add_argument("--qp-tol", type=float, default=1e-10,
                     help="IPM stopping tolerance of the QPs (default 1e-10; 1e-8 = Clarabel's default, which "
                          "the reference runs with)")
@@ -529,8 +532,18 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     def step(k):
         L.check(lib.dat_control_step(h, None, L.ptr(accs[k % ACC_POOL]), None, None, None, None, None, None))
 
-    for k in range(args.warmup):
-        step(k)
+    def fused(k0, K):
+        seq = L.f64(np.stack([accs[(k0 + k) % ACC_POOL] for k in range(K)]))
+        L.check(lib.dat_control_steps(h, K, L.ptr(seq), None, None, None))
+
+    if args.fused and args.mode == "centralized":
+        sys.exit("bench.py: --fused covers the C-ADMM / DD configs")
+    if args.fused:
+        if args.warmup:
+            fused(0, args.warmup)
+    else:
+        for k in range(args.warmup):
+            step(k)
     eng.synchronize()
     eng.reset_counters()
 
@@ -543,13 +556,17 @@ def qp_level(args, dist, rank: int, world: int, local: int):
 
     barrier()
     eng.synchronize()
-    per_step = np.empty(args.steps)
+    per_step = np.full(args.steps, np.nan)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ts = time.perf_counter()
-        step(args.warmup + k)
+    if args.fused:  # (the K x B x 6 host-to-device copy of the acc sequence is inside the timed region)
+        fused(args.warmup, args.steps)
         eng.synchronize()
-        per_step[k] = (time.perf_counter() - ts) * 1e3
+    else:
+        for k in range(args.steps):
+            ts = time.perf_counter()
+            step(args.warmup + k)
+            eng.synchronize()
+            per_step[k] = (time.perf_counter() - ts) * 1e3
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -578,12 +595,15 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     if args.mode == "centralized":
         work_mode = "one centralized QP per scenario and step"
     workload = f"{cfg}: {args.mode} n={n}, QP-level, no env ({work_mode}), {B} scenarios per GPU"
+    if args.fused:
+        workload += f", {args.steps} control steps fused into one drain (dat_control_steps)"
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
         "value": qps / elapsed, "unit": "centralized-QP solves/s" if args.mode == "centralized" else "agent-QP solves/s",
         "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "ms_per_step_p50": float(np.percentile(per_step, 50)), "ms_per_step_p99": float(np.percentile(per_step, 99)),
+        "ms_per_step_p50": None if args.fused else float(np.percentile(per_step, 50)),
+        "ms_per_step_p99": None if args.fused else float(np.percentile(per_step, 99)),
         "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (perturbed rest states, acc_des ~ U(-5,5)^6" + (", randomized payload mass/inertia)" if per_scen else ")"),

@@ -18,4 +18,8 @@ for c in ${CONFIGS:-C1 C2 C3 C5}; do
   timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline > $O/bench_$c.log 2>&1 || { tail -30 $O/bench_$c.log; exit 14; }
   python tools/show_bench.py $O/bench_$c.log; grep -o "\"inband[^,]*,[^,]*" $O/bench_$c.log
 done
+for c in ${FUSED:-}; do
+  timeout -k 10 300 python -u bench.py --config $c --fused --steps ${FSTEPS:-10} --no-cpu-baseline > $O/bench_${c}_fused.log 2>&1 || { tail -30 $O/bench_${c}_fused.log; exit 15; }
+  python tools/show_bench.py $O/bench_${c}_fused.log; grep -o "\"inband[^,]*,[^,]*" $O/bench_${c}_fused.log
+done
 echo done
