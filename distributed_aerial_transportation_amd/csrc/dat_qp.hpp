@@ -197,8 +197,13 @@ DAT_HD constexpr int best_size(int NB) { return 3 * NB + 18; }
 // ------------------------------------------------------------------ shared data
 // k_f, k_m: total force / moment weights; variants: bit 0 build C[0] (kdv = 0), bit 1 build C[1]
 // (kdv = 1).  with_K: C-ADMM aggregate over all agents.
-DAT_HD void build_shared(QPShared& S, const double* prm, int n, const double* st, const double* acc, double k_f,
-                         double k_m, int variants, bool with_K) {
+// Not inlined: the drains call it from two sites (a slot's new scenario, and a fused next step,
+// dat_control_steps), and one compiled body keeps the two bitwise identical (inlined copies may contract
+// multiply-adds differently).  Once per scenario and step: the call costs nothing measurable.
+__host__ __device__ inline __attribute__((noinline)) void build_shared(QPShared& S, const double* prm, int n,
+                                                                        const double* st, const double* acc,
+                                                                        double k_f, double k_m, int variants,
+                                                                        bool with_K) {
   const double mT = prm[DAT_P_MT];
   const double* xc = prm + DAT_P_XCOM;
   const double* JT = prm + DAT_P_JT;
