@@ -104,6 +104,9 @@ def parse():
     ap.add_argument("--fused", action="store_true",
                     help="C2/C3/C5: the timed steps as ONE dat_control_steps call (each scenario starts its next "
                          "control step as soon as its previous one ends; ms_per_step = elapsed / steps)")
+    ap.add_argument("--sub-batches", type=int, default=1,
+                    help="C4: run each GPU's scenarios as this many sub-batches on their own streams "
+                         "(dat_set_sub_batches; per-scenario arithmetic unchanged)")
     ap.add_argument("--qp-tol", type=float, default=1e-10,
                     help="IPM stopping tolerance of the QPs (default 1e-10; 1e-8 = Clarabel's default, which "
                          "the reference runs with)")
@@ -408,6 +411,8 @@ def main():
         eng.set_qp_tolerance(args.qp_tol)
         eng.set_forests(forests, scen_forest)
         eng.set_state(states, np.zeros(B, dtype=np.int32))
+        if args.sub_batches > 1:
+            eng.set_sub_batches(args.sub_batches)
     eng.closed_loop(args.warmup)
     eng.reset_counters()
 
@@ -461,6 +466,10 @@ def main():
                                     "admm_slot_utilisation": w["qp_solves"] / n / max(w["wave_admm_iters"], 1)}
             k_ms = w["kernel_ms"]
     kernel_ms = k_ms / max(hl_steps, 1)
+    if args.sub_batches > 1:
+        # the sub-batches' kernels overlap on their streams: no per-launch span of k_cadmm exists, so the
+        # rate is taken over the whole step's device time (a lower bound on the k_cadmm rate)
+        kernel = f"k_cadmm + step kernels ({args.sub_batches} sub-batch streams, whole-step device time)"
     flops_launch = model_flops(args.mode, n, k_ipm, k_row, work.get("refine_passes", 0),
                                work.get("refine_corrections", 0)) / max(hl_steps, 1)
     achieved_tflops = flops_launch / max(kernel_ms * 1e-3, 1e-12) / 1e12
@@ -488,7 +497,8 @@ def main():
                  f"synthetic (seeded forests 0..63, randomized C4 {args.start} start states)"),
         "config": {"workload": workload,
                    "n": n, "scenarios_per_gpu": B, "total_scenarios": scen_all, "hl_every": 10, "dt": 1e-3,
-                   "qp_tol": args.qp_tol, "parallelism": f"scenario-sharded x{world}"},
+                   "qp_tol": args.qp_tol, "parallelism": f"scenario-sharded x{world}",
+                   "sub_batches": args.sub_batches},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
                   "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),

@@ -148,6 +148,7 @@ EXPORTS = {
     "dat_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_closed_loop": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_control_steps": (ctypes.c_int, [H, ctypes.c_int, D, D, I, I]),
+    "dat_set_sub_batches": (ctypes.c_int, [H, ctypes.c_int]),
     "dat_get_step_marks": (ctypes.c_int, [H, D, ctypes.c_int]),
     "dat_get_counters": (ctypes.c_int, [H, LL, LL, LL, LL, D]),
     "dat_get_class_counters": (ctypes.c_int, [H, ctypes.c_int, LL, LL, LL, D]),

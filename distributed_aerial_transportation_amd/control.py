@@ -202,6 +202,10 @@ class BatchedController:
             fd = L.f64(np.asarray(f).transpose(0, 2, 1).reshape(self.batch, 3 * self.n))
         L.check(self._lib.dat_rp_rollout(self._h, int(steps), L.ptr(fd)))
 
+    def set_sub_batches(self, count: int) -> None:
+        """dat_set_sub_batches: closed_loop on `count` sub-batches with one stream each (C-ADMM)."""
+        L.check(self._lib.dat_set_sub_batches(self._h, int(count)))
+
     def closed_loop(self, hl_steps: int) -> None:
         L.check(self._lib.dat_closed_loop(self._h, int(hl_steps)))
 

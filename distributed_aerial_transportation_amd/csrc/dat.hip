@@ -1654,6 +1654,7 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
 // ================================================================================================
 // handle + C-ABI
 // ================================================================================================
+constexpr int DAT_MAX_SUB = 4;  // sub-batches of the C-ADMM closed loop (dat_set_sub_batches)
 struct dat_handle {
   dat_config cfg;
   int P = 0, S = 0;
@@ -1692,6 +1693,12 @@ struct dat_handle {
   std::vector<double> marks;
   double* acc_seq = nullptr;  // dat_control_steps: K x B x 6 desired accelerations (grown on demand)
   size_t acc_seq_cap = 0;
+  // C-ADMM closed loop on sub-batches (dat_set_sub_batches): contiguous scenario ranges, each with its own
+  // stream, so one sub-batch's kernels fill the drain tail and the short kernels of the others
+  int nsub = 1;
+  hipStream_t sub_stream[DAT_MAX_SUB] = {};
+  hipEvent_t sub_done[DAT_MAX_SUB] = {};
+  hipEvent_t ev_start = nullptr, ev_end = nullptr;
   double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
@@ -1845,6 +1852,41 @@ int launch_hl(dat_handle* h, int ksteps = 1, const double* acc_seq = nullptr) {
   return 0;
 }
 
+// kernel arguments of the C-ADMM sub-batch of scenarios [off, off + Bs) (dat_set_sub_batches): every
+// per-scenario array offset, the env-row image a disjoint block of the SoA buffer (stride Bs n), the
+// class table its own; counters shared (atomics)
+template <class T>
+T* offp(T* p, size_t k) { return p ? p + k : p; }
+KArgs sub_kargs(dat_handle* h, int off, int Bs, int s) {
+  KArgs a = kargs(h);
+  const size_t n = h->cfg.n, N3 = 3 * n, o = (size_t)off;
+  a.B = Bs;
+  a.G = cadmm_slots(h, Bs, (int)n);
+  if (a.ppp) a.params += o * a.P;
+  a.state += o * a.S;
+  a.counter += o;
+  a.acc += o * 6;
+  a.fdes += o * N3;
+  a.scen_forest = offp(a.scen_forest, o);
+  a.cf += o * n * N3;
+  a.cfbar += o * N3;
+  a.clam += o * n * N3;
+  a.best += o * n * best_size(1);
+  a.iters += o;
+  a.qstatus += o * n;
+  a.mind += o;
+  a.col += o;
+  a.err = offp(a.err, o * (a.max_iter + 1));
+  a.need += o;
+  a.ipmx += o;
+  a.slist += o;
+  a.scount = h->scount + 3 * NCLS * s;
+  a.qhead = a.scount + 2 * NCLS;
+  a.erows += (size_t)4 * DAT_NENV * n * o;
+  a.emask += o * n;
+  return a;
+}
+
 int finish_hl(dat_handle* h, int ksteps = 1) {
   HIPCHK(hipEventSynchronize(h->e1));
   float ms = 0.f;
@@ -1955,7 +1997,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->erows, (size_t)B * n * DAT_NENV * 4);
     rc |= dalloc(h, &h->emask, (size_t)B * n);
     rc |= dalloc(h, &h->slist, B);
-    rc |= dalloc(h, &h->scount, 3 * NCLS);
+    rc |= dalloc(h, &h->scount, 3 * NCLS * DAT_MAX_SUB);  // one class table per sub-batch
     rc |= dalloc(h, &h->cf, B * n * N3);
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
@@ -1996,6 +2038,12 @@ int dat_destroy(dat_handle* h) {
   for (void* p : h->allocs)
     if (p) (void)hipFree(p);
   if (h->acc_seq) (void)hipFree(h->acc_seq);
+  for (int s = 1; s < DAT_MAX_SUB; ++s) {
+    if (h->sub_stream[s]) (void)hipStreamDestroy(h->sub_stream[s]);
+    if (h->sub_done[s]) (void)hipEventDestroy(h->sub_done[s]);
+  }
+  if (h->ev_start) (void)hipEventDestroy(h->ev_start);
+  if (h->ev_end) (void)hipEventDestroy(h->ev_end);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
   if (h->ek) (void)hipEventDestroy(h->ek);
@@ -2197,9 +2245,57 @@ int dat_rollout(dat_handle* h, int steps, const double* f_des) {
   return 0;
 }
 
+// the closed loop on sub-batches: hl_steps x (desired acceleration, env classes, class sort, C-ADMM drain,
+// rollout) per sub-batch on its own stream, no synchronisation between the sub-batches or the steps
+int closed_loop_sub(dat_handle* h, int hl_steps) {
+  if (!h->have_params) return fail("dat_set_params has not been called");
+  const int B = h->cfg.batch, n = h->cfg.n, S = h->nsub;
+  auto now_ms = [] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  h->marks.clear();
+  h->marks.push_back(now_ms());
+  HIPCHK(hipEventRecord(h->ev_start, h->stream));
+  for (int s = 1; s < S; ++s) HIPCHK(hipStreamWaitEvent(h->sub_stream[s], h->ev_start, 0));
+  for (int k = 0; k < hl_steps; ++k) {
+    for (int s = 0; s < S; ++s) {
+      const int off = (int)((long long)B * s / S), Bs = (int)((long long)B * (s + 1) / S) - off;
+      hipStream_t st = h->sub_stream[s];
+      KArgs a = sub_kargs(h, off, Bs, s);
+      hipLaunchKernelGGL(k_desired, dim3((Bs + 63) / 64), dim3(64), 0, st, a, (double*)a.acc);
+      const int G = 64 / n;
+      hipLaunchKernelGGL(k_env_class, dim3((Bs + G - 1) / G), dim3(64), 0, st, a);
+      hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, st, Bs, (const int*)a.need, a.slist, a.scount);
+      hipLaunchKernelGGL(k_cadmm, dim3(std::min((Bs + a.G - 1) / a.G, h->persistent_blocks)), dim3(64),
+                         cadmm_lds_bytes(n, a.G, h->nforest > 0 ? NCLS - 1 : 0), st, a);
+      launch_rollout(a, Bs, st, h->cfg.hl_every, h->cfg.dt, (const double*)a.fdes);
+      HIPCHK(hipGetLastError());
+    }
+  }
+  for (int s = 1; s < S; ++s) {
+    HIPCHK(hipEventRecord(h->sub_done[s], h->sub_stream[s]));
+    HIPCHK(hipStreamWaitEvent(h->stream, h->sub_done[s], 0));
+  }
+  HIPCHK(hipEventRecord(h->ev_end, h->stream));
+  HIPCHK(hipEventSynchronize(h->ev_end));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, h->ev_start, h->ev_end));
+  // the whole run's device time (the sub-batches' kernels overlap: no per-kernel span)
+  h->hl_ms += ms;
+  h->cadmm_ms += ms;
+  h->hl_steps += hl_steps;
+  h->marks.push_back(now_ms());
+  return 0;
+}
+
 int dat_closed_loop(dat_handle* h, int hl_steps) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
+  if (h->nsub > 1) {
+    if (closed_loop_sub(h, hl_steps)) return -1;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+  }
   const size_t B = h->cfg.batch;
   KArgs a = kargs(h);
   auto now_ms = [] {
@@ -2295,6 +2391,24 @@ int dat_reset_counters(dat_handle* h) {
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
   h->hl_ms = 0.0;
+  return 0;
+}
+
+int dat_set_sub_batches(dat_handle* h, int count) {
+  if (!h) return fail("null handle");
+  if (count < 1 || count > DAT_MAX_SUB) return fail("dat_set_sub_batches: count must be in [1, 4]");
+  if (count > 1 && h->cfg.mode != DAT_MODE_CADMM) return fail("dat_set_sub_batches: C-ADMM handles only");
+  if (count > h->cfg.batch) return fail("dat_set_sub_batches: more sub-batches than scenarios");
+  if (count > 1 && h->cfg.record_err) return fail("dat_set_sub_batches: record_err must be 0");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  h->sub_stream[0] = h->stream;
+  for (int s = 1; s < count; ++s) {
+    if (!h->sub_stream[s]) HIPCHK(hipStreamCreateWithFlags(&h->sub_stream[s], hipStreamNonBlocking));
+    if (!h->sub_done[s]) HIPCHK(hipEventCreateWithFlags(&h->sub_done[s], hipEventDisableTiming));
+  }
+  if (!h->ev_start) HIPCHK(hipEventCreate(&h->ev_start));
+  if (!h->ev_end) HIPCHK(hipEventCreate(&h->ev_end));
+  h->nsub = count;
   return 0;
 }
 

@@ -141,6 +141,11 @@ int dat_rp_rollout(dat_handle* h, int steps, const double* f);
  * acceleration of :33-59): hl_steps x (desired acceleration + control step +
  * hl_every rollout steps); inputs already in HBM, nothing copied per step. */
 int dat_closed_loop(dat_handle* h, int hl_steps);
+/* C-ADMM handles: run dat_closed_loop on `count` (1..4) contiguous sub-batches of the scenarios, each on
+ * its own stream with no synchronisation between sub-batches or steps, so that one sub-batch's kernels
+ * fill the others' drain tails and short kernels.  Per scenario the arithmetic is unchanged (a scenario's
+ * results never depend on the grouping).  count = 1 (default) restores the single-stream loop. */
+int dat_set_sub_batches(dat_handle* h, int count);
 /* Host steady-clock marks (ms) of the last dat_closed_loop call: [0] its start (0.0), then the completion
  * of each HL step's control kernel; consecutive differences are per-step times of the back-to-back run.
  * Writes up to max_marks values; returns the number of marks (hl_steps + 1). */

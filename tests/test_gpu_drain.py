@@ -160,10 +160,13 @@ def test_gpu_fused_steps_equal_separate_steps(mode, n, B, blocks):
     rng = np.random.default_rng(500 + n)
     states = scenarios.perturbed_states(n, B, rng)
     accs = rng.uniform(-0.5, 0.5, (K, B, 6)) * 8.0
+    # (the same grid cap on both sides: a C-ADMM wavefront's slot count G follows the grid, and G selects
+    # where the class's IPM state lives -- registers or LDS -- i.e. another compiled instantiation)
     sep = BatchedController(mode, n, B, scenarios.params_block(n))
+    sep.set_persistent_blocks(blocks)
     sep.set_state(states)
     seps = [sep.control(None, accs[k]) for k in range(K)]
-    # (the separate path against itself on another handle and grid: run-to-run / grouping independence)
+    # the separate path against itself on another handle: run-to-run determinism
     sep2 = BatchedController(mode, n, B, scenarios.params_block(n))
     sep2.set_persistent_blocks(blocks)
     sep2.set_state(states)
@@ -184,3 +187,30 @@ def test_gpu_fused_steps_equal_separate_steps(mode, n, B, blocks):
         assert np.array_equal(r_fus.qp_status, r_sep.qp_status)
         fus.close()
     assert sep.work()["hl_steps"] == K
+
+
+@pytest.mark.parametrize("subs", [2, 3])
+def test_gpu_closed_loop_sub_batches_bitwise(subs):
+    """dat_set_sub_batches: the C4 closed loop (desired acceleration, env classes, class sort, C-ADMM drain,
+    rollout) on 2 or 3 sub-batches, each on its own stream with no synchronisation between them, must
+    leave every scenario in exactly the state of the single-stream loop after 3 HL steps (a scenario's
+    arithmetic does not depend on its grouping), with the same work counters."""
+    from distributed_aerial_transportation_amd import BatchedController, Forest, scenarios
+    from tests.test_gpu_c4 import near_tree_states
+
+    n, B, K = 6, 131, 3
+    forests = [Forest.seeded(s) for s in range(4)]
+    sf = np.arange(B) % 4
+    x0 = near_tree_states(n, forests, sf, np.random.default_rng(77))
+    out = []
+    for sb in (1, subs):
+        eng = BatchedController("cadmm", n, B, scenarios.params_block(n))
+        eng.set_forests(forests, sf)
+        eng.set_state(x0, np.zeros(B, dtype=np.int32))
+        eng.set_sub_batches(sb)
+        eng.closed_loop(K)
+        st, _ = eng.get_state()
+        out.append((st, eng.work()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    for key in ("qp_solves", "ipm_iters", "ipm_row_iters", "hl_steps"):
+        assert out[0][1][key] == out[1][1][key], key
