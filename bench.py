@@ -229,12 +229,14 @@ def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: in
     except (OSError, IndexError):
         cpu = "unknown"
     return {"value": qN / tN, "unit": "agent-QP solves/s", "cores": threads, "affinity_cpus": affinity,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "kind": "port", "single_core_value": q1 / t1, "ipm_iters_per_qp": iN / max(qN, 1),
             "sample": f"C++ OpenMP restatement of the C4 loop (cpu_baseline/dat_cpu.hip, same per-lane code as the "
                       f"kernels), n={n}: the first {S} of the bench's {batch} {start}-start scenarios (rank 0), "
                       f"{warmup} untimed + {steps} timed HL steps like the GPU line ({qN} agent QPs, "
-                      f"{iN / max(qN, 1):.2f} IPM it/QP, {tN:.1f} s) on {threads} OpenMP threads (the box's CPU "
-                      f"share; sched_getaffinity: {affinity} CPUs); 1 thread: {S1} scenarios x {steps} steps "
+                      f"{iN / max(qN, 1):.2f} IPM it/QP, {tN:.1f} s) on {threads} OpenMP threads "
+                      f"(omp_get_max_threads, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}: the "
+                      f"box's CPU share; sched_getaffinity: {affinity} CPUs); 1 thread: {S1} scenarios x {steps} steps "
                       f"({q1} QPs); host CPU {cpu}, os.cpu_count() {os.cpu_count()}"}
 
 
