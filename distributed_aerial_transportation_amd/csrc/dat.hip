@@ -67,24 +67,29 @@ int fail(const std::string& m) {
 // stride in doubles so that the 32 lanes of a ds_read_b64 group fall on distinct bank pairs.
 //   fbar G x 3n    consensus mean
 //   Rt   G x 9n    hat(r_com_j) Rl'
-//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)            done / sid 64 + 64 ints
+//   sh   G x QPShared (u-maps, packed Hessians, base rows, K)            done / sid / wmx: G ints each
 //   area, laid out per env class:
 //     rows  the IPM's row state (RowLds: s, z, zw of NR slots x 64 lanes, 3 NR x 64 doubles); the
 //           consensus exchange slots red (64 x RDS) alias it: they are used only between solves
 //     env   EnvLdsN image of the class's env slots (structure of arrays over the 64 lanes)
 // The row state goes to LDS for classes 1 and 2 when their image fits the 40 KB a wavefront may
 // hold at four wavefronts per CU (cadmm_rows_lds); class 0 (3 slots) and class 3 (13 slots) keep it
-// in registers.  n = 6: class 0 19.9 KB, 1 27.1 KB, 2 37.8 KB, 3 40.4 KB (C4 A/B, k_cadmm ms:
-// rows of classes 0-2 in LDS 5.53, classes 1-2 5.45, class 2 only 5.51).
-constexpr int RDS = 9;
+// in registers.  n = 6: class 0 35.3 KB (rows + aux slots), 1 27.9 KB, 2 38.4 KB, 3 39.3 KB (C4 A/B,
+// k_cadmm ms: rows of classes 0-2 in LDS 5.53, classes 1-2 5.45, class 2 only 5.51).  Round 4 trimmed
+// the exchange slots (RDS 9 -> 7) and the per-slot ints (3 x 64 -> 3 G): class 3's carve was 41.9 KB,
+// which with the 256 B of static LDS left room for three workgroups per CU (one SIMD idle); four fit now
+// (C4 A/B 3.83 / 3.80 -> 3.72 / 3.77 ms per step).
+constexpr int RDS = 7;  // consensus exchange slots per lane: mean (3) or F / M totals (6), total residual at [6]
 constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
 // G: scenario slots per wavefront (cadmm_slots)
 // doubles rounded up to a 16-byte multiple: every LDS region starts 16-byte aligned (pair reads)
 __host__ __device__ constexpr size_t al2(size_t d) { return (d + 1) & ~(size_t)1; }
+// per-slot ints done / sid / wmx (G each), rounded to 16 bytes
+__host__ __device__ constexpr int slot_ints(int G) { return (3 * G + 3) & ~3; }
 __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
   return sizeof(double) * (al2((size_t)G * 3 * n) + (size_t)G * RT_STRIDE * n) + sizeof(QPShared) * (size_t)G +
-         sizeof(int) * 192;
+         sizeof(int) * (size_t)slot_ints(G);
 }
 // IPM per-iteration quantities moved to LDS aux slots (ipm_solve AUXM) per env class, when the class's
 // carve still fits the budget: class 0 all groups (its 3 row slots leave room; class-0 probe scratch
@@ -150,9 +155,9 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.Rt = L.fbar + al2(G * 3 * n);
   L.sh = (QPShared*)(L.Rt + G * RT_STRIDE * n);
   L.done = (int*)(L.sh + G);
-  L.sid = L.done + 64;
-  L.wmx = L.sid + 64;
-  L.rows = (double*)(L.wmx + 64);
+  L.sid = L.done + G;
+  L.wmx = L.sid + G;
+  L.rows = (double*)(L.done + slot_ints(G));
   L.red = L.rows;
   const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
