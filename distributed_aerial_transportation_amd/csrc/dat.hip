@@ -74,7 +74,7 @@ int fail(const std::string& m) {
 //     env   EnvLdsN image of the class's env slots (structure of arrays over the 64 lanes)
 // The row state goes to LDS for classes 1 and 2 when their image fits the 40 KB a wavefront may
 // hold at four wavefronts per CU (cadmm_rows_lds); class 0 (3 slots) and class 3 (13 slots) keep it
-// in registers.  n = 6: class 0 35.3 KB (rows + aux slots), 1 27.9 KB, 2 38.4 KB, 3 39.3 KB (C4 A/B,
+// in registers.  n = 6: class 0 34.8 KB (rows + aux slots), 1 27.3 KB, 2 37.8 KB, 3 39.3 KB (C4 A/B,
 // k_cadmm ms: rows of classes 0-2 in LDS 5.53, classes 1-2 5.45, class 2 only 5.51).  Round 4 trimmed
 // the exchange slots (RDS 9 -> 7) and the per-slot ints (3 x 64 -> 3 G): class 3's carve was 41.9 KB,
 // which with the 256 B of static LDS left room for three workgroups per CU (one SIMD idle); four fit now
