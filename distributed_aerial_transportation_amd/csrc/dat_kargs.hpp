@@ -39,7 +39,7 @@ constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
 // IPM refinement passes run and corrections applied (all kernels; the executed-flop model)
 constexpr int CNT_REF = CNT_INBAND + 2;
 constexpr int DAT_NCOUNTERS = CNT_REF + 2;
-constexpr double INBAND_CLARABEL = 1e-8;
+constexpr double INBAND_CLARABEL = IPM_CLARABEL_TOL;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
 
 struct KArgs {

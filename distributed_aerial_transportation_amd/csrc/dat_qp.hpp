@@ -193,6 +193,8 @@ DAT_HD int rows_needed(unsigned emask) { return NBASE + (emask ? 32 - __builtin_
 
 // size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6)
 DAT_HD constexpr int best_size(int NB) { return 3 * NB + 18; }
+// Clarabel's own tolerance: an in-band exit whose merit is above it is one Clarabel would not certify
+constexpr double IPM_CLARABEL_TOL = 1e-8;
 
 // ------------------------------------------------------------------ shared data
 // k_f, k_m: total force / moment weights; variants: bit 0 build C[0] (kdv = 0), bit 1 build C[1]
@@ -711,7 +713,7 @@ struct IPMOut {
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP>
 DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
-                          bool tuned) {
+                          int start) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   // aux slot offsets (only the AUXM groups are allocated)
   constexpr int O_SC = 0;
@@ -914,9 +916,12 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
   // inputs and 17-28 passes: the tuned start everywhere took C2 13 -> 20 ms and C5 81 -> 118 ms per
   // step), DD agent QPs (C3 29 -> 39 ms) and the centralized QP (also the rigid payload on the same
   // kernel, whose Jl^-1 ~ 50 grades the Newton systems)
-  const bool TUNED = MODE == MODE_CADMM && tuned;
-  const double S0 = TUNED ? DAT_IPM_S0 : MODE == MODE_DD ? DAT_DD_S0 : 1.0;
-  const double Z0 = TUNED ? DAT_IPM_Z0 : MODE == MODE_DD ? DAT_DD_Z0 : 1.0;
+  // start 0: conservative (as above), 1: tuned (C-ADMM), 2: the conservative start scaled by 10 (the
+  // second start of a DD / centralized solve that ended outside Clarabel's tolerance, see ipm_solve)
+  const bool TUNED = MODE == MODE_CADMM && start == 1;
+  const double SCL = start == 2 ? 10.0 : 1.0;
+  const double S0 = SCL * (TUNED ? DAT_IPM_S0 : MODE == MODE_DD ? DAT_DD_S0 : 1.0);
+  const double Z0 = SCL * (TUNED ? DAT_IPM_Z0 : MODE == MODE_DD ? DAT_DD_Z0 : 1.0);
   const double ETA = TUNED ? DAT_IPM_ETA : MODE == MODE_DD ? DAT_DD_ETA : 0.99;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
@@ -1757,24 +1762,39 @@ template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = Row
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
                         GRP grp = GRP{}) {
-  bool tuned = MODE == MODE_CADMM && P.tuned;
-  int done = 0, done_refs = 0, done_corrs = 0;
+  // First start: tuned for the C-ADMM agent QPs of the warm closed loop (P.tuned), conservative otherwise.
+  // A tuned attempt that does not converge cleanly is redone from the conservative start (a tuned attempt
+  // that has not converged in 20 iterations is not converging: C4's tuned solves take 4.3 on average and
+  // at most ~10).  A conservative attempt accepted through an in-band iterate outside Clarabel's 1e-8
+  // (rounding-path accidents, ~1 agent QP in 10^7 on C5 and C1: the same QPs on the host build converge
+  // from either start) is redone from another start (C-ADMM: tuned; DD / centralized: the conservative
+  // start scaled by 10), whose result is taken.  (Not the attempts that end with no in-band iterate:
+  // they already ran to max_iter, and a second 50 iterations lengthened C1's slowest wavefront by 45 %.)  One call site
+  // and two ints of loop state: every ipm_attempt instantiation is inlined once (a save / compare /
+  // restore of the first result cost k_cadmm 4 % and k_cent 50 % in register pressure, round 4).
+  const int first = MODE == MODE_CADMM && P.tuned ? 1 : 0;
+  int start = first, second = 0, done = 0, done_refs = 0, done_corrs = 0;
   IPMOut o;
 #pragma unroll 1
   for (;;) {
-    // (a tuned attempt that has not converged in 20 iterations is not converging: C4's tuned solves take
-    // 4.3 on average and at most ~10)
     o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP>(sh, er, rt, P, y0, y, w, best,
-                                                             tuned && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
-                                                             tuned);
+                                                             start == 1 && !second && max_iter > 20 ? 20 : max_iter,
+                                                             tol, rw, grp, start);
     o.iters += done;
     o.refs += done_refs;
     o.corrs += done_corrs;
-    if (!tuned || (o.why == 0 && !o.inband) || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
+    if (second || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
+    if (start == 1) {
+      if (o.why == 0 && !o.inband) break;
+      start = 0;
+    } else {
+      if (!(o.status == ST_OPTIMAL && o.inband && o.merit > IPM_CLARABEL_TOL)) break;
+      start = MODE == MODE_CADMM ? 1 : 2;
+    }
+    second = 1;
     done = o.iters;
     done_refs = o.refs;
     done_corrs = o.corrs;
-    tuned = false;
   }
   return o;
 }

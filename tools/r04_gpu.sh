@@ -7,7 +7,7 @@ cd $R && mkdir -p gpurun_out
 O=gpurun_out
 export PYTHONUNBUFFERED=1
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail=${MAXFAIL:-1} -v --timeout 300 --timeout-method thread ${PYARGS:-} > $O/gpu_tests.log 2>&1 || { tail -60 $O/gpu_tests.log; exit 11; }
+  timeout -k 10 1080 python -u -m pytest tests -m gpu --maxfail=${MAXFAIL:-1} -v --timeout 300 --timeout-method thread ${PYARGS:-} > $O/gpu_tests.log 2>&1 || { tail -60 $O/gpu_tests.log; exit 11; }
   tail -3 $O/gpu_tests.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 12; }
   tail -1 $O/smoke.log
