@@ -77,10 +77,14 @@ int fail(const std::string& m) {
 // in registers.  n = 6: class 0 34.8 KB (rows + aux slots), 1 27.3 KB, 2 37.8 KB, 3 39.3 KB (C4 A/B,
 // k_cadmm ms: rows of classes 0-2 in LDS 5.53, classes 1-2 5.45, class 2 only 5.51).  Round 4 trimmed
 // the exchange slots (RDS 9 -> 7) and the per-slot ints (3 x 64 -> 3 G): class 3's carve was 41.9 KB,
-// which with the 256 B of static LDS left room for three workgroups per CU (one SIMD idle); four fit now
-// (C4 A/B 3.83 / 3.80 -> 3.72 / 3.77 ms per step).
+// which with the 256 B of static LDS left room for three workgroups per CU (one SIMD idle); four fit after
+// the trim (C4 A/B 3.83 / 3.80 -> 3.72 / 3.77 ms per step), and the budget then went to classes 1 and 2's
+// aux groups at three per CU instead (LDS_WAVE_BUDGET).
 constexpr int RDS = 7;  // consensus exchange slots per lane: mean (3) or F / M totals (6), total residual at [6]
-constexpr size_t LDS_WAVE_BUDGET = 40 * 1024;
+// LDS budget of one k_cadmm workgroup: 53 KB = three per CU.  Four per CU (40 KB) bought ~2 % (§5 of
+// DESIGN.md, round 4); the 13 KB more per workgroup hold classes 1 and 2's IPM aux groups in LDS
+// instead (C4 A/B 3.79 / 3.80 -> 3.75 / 3.74 ms per step).
+constexpr size_t LDS_WAVE_BUDGET = 53 * 1024;
 __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_rows(cls); }
 // G: scenario slots per wavefront (cadmm_slots)
 // doubles rounded up to a 16-byte multiple: every LDS region starts 16-byte aligned (pair reads)
@@ -94,22 +98,11 @@ __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
 // IPM per-iteration quantities moved to LDS aux slots (ipm_solve AUXM) per env class, when the class's
 // carve still fits the budget: class 0 all groups (its 3 row slots leave room; class-0 probe scratch
 // traffic 145 -> 23 ops per IPM pass; A/B on MI355X: C2 12.1 -> 11.0 ms, C5 80.7 -> 73.2 ms per step);
-// classes 1 and 2 none (lambda alone in class 1: C4 3.66 vs 3.67 ms, no gain; class 2's 5 env rows
-// fill the budget).
+// classes 1 and 2 all groups since round 4, at three workgroups per CU (LDS_WAVE_BUDGET; class 3's 13
+// row slots do not fit).
 // C-ADMM consensus mean and residual read agent-major, the three components of a block together
 // (bitwise equal to the component-major loops; C4 A/B: k_cadmm 3.68 / 3.63 -> 3.57 / 3.54 ms)
-#ifndef DAT_AUXM0
-#define DAT_AUXM0 15
-#endif
-#ifndef DAT_AUXM1
-#define DAT_AUXM1 0
-#endif
-#ifndef DAT_AUXM2
-#define DAT_AUXM2 0
-#endif
-__host__ __device__ constexpr unsigned cadmm_auxm(int cls) {
-  return cls == 0 ? DAT_AUXM0 : cls == 1 ? DAT_AUXM1 : cls == 2 ? DAT_AUXM2 : 0u;
-}
+__host__ __device__ constexpr unsigned cadmm_auxm(int cls) { return cls < NCLS - 1 ? 15u : 0u; }
 // row-state placement of a class: 0 registers, 1 LDS rows, 2 LDS rows + aux slots
 __host__ __device__ inline size_t cadmm_area_doubles(int cls, int rmode) {
   const size_t rows = rmode ? (size_t)row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
