@@ -249,10 +249,10 @@ def shard(rank: int, batch: int, num_forests: int):
 
 def strong_shard(rank: int, world: int, total: int):
     """Strong scaling: contiguous split of `total` scenario ids over `world` ranks (the first
-    total % world ranks take one more)."""
-    base, extra = divmod(total, world)
-    lo = rank * base + min(rank, extra)
-    return lo, base + (1 if rank < extra else 0)
+    total % world ranks take one more): the package's sharding.shard_range."""
+    from distributed_aerial_transportation_amd.sharding import shard_range
+
+    return shard_range(rank, world, total)
 
 
 def bench_states(n: int, batch: int, rank: int, world: int, forests_n: int, start: str, total):
@@ -280,18 +280,13 @@ def bench_states(n: int, batch: int, rank: int, world: int, forests_n: int, star
 
 
 def combine_ranks(dist, world: int, tot: np.ndarray, metrics: np.ndarray, device):
-    """Sum of the work counters, max of the elapsed time, all-gather of the per-scenario metrics.
-    The only collectives of the run (RCCL over xGMI with the nccl backend; gloo on CPU in tests)."""
-    import torch
+    """Sum of the work counters, max of the elapsed time, all-gather of the per-scenario metrics (uneven
+    shards included) through the package's sharding collectives.  The only collectives of the run (RCCL
+    over xGMI with the nccl backend; gloo on CPU in tests)."""
+    from distributed_aerial_transportation_amd.sharding import gather_rows, reduce_values
 
-    t = torch.tensor(tot, dtype=torch.float64, device=device)
-    mx = t.clone()
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    gm = torch.tensor(metrics, dtype=torch.float64, device=device)
-    gath = [torch.empty_like(gm) for _ in range(world)]
-    dist.all_gather(gath, gm)
-    return t.cpu().numpy(), mx.cpu().numpy(), torch.cat(gath).cpu().numpy()
+    return (reduce_values(tot, "sum", device), reduce_values(tot, "max", device),
+            gather_rows(metrics, device))
 
 
 def spawn_ranks(args) -> int:
