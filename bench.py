@@ -80,6 +80,15 @@ def traffic_per_launch(kernel: str, workload: str):
     return e["bytes_per_launch"], e.get("source")
 
 
+def auto_sub_batches(per_gpu: int) -> int:
+    """C4 stream count per GPU.  A drain of 65,536 scenarios fills the chip and its tail is short (4 streams:
+    3.73 -> 3.49 ms per step, +6 %, and the per-launch roofline would then split over 4 concurrent launches);
+    at the per-GPU batches of the 2-, 4- and 8-GPU splits the slowest scenarios' passes dominate each step
+    and 4 streams overlap one sub-batch's tail with the others' work: 32,768 3.06 -> 2.69, 16,384
+    2.62 -> 2.20, 8,192 2.24 -> 1.82 ms per step (round 4 A/B, tools/r04_subs.sh)."""
+    return 1 if per_gpu >= 65536 else 4
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,9 +113,10 @@ def parse():
     ap.add_argument("--fused", action="store_true",
                     help="C2/C3/C5: the timed steps as ONE dat_control_steps call (each scenario starts its next "
                          "control step as soon as its previous one ends; ms_per_step = elapsed / steps)")
-    ap.add_argument("--sub-batches", type=int, default=1,
+    ap.add_argument("--sub-batches", type=int, default=None,
                     help="C4: run each GPU's scenarios as this many sub-batches on their own streams "
-                         "(dat_set_sub_batches; per-scenario arithmetic unchanged)")
+                         "(dat_set_sub_batches; per-scenario arithmetic unchanged).  Default: 1 when a GPU holds "
+                         ">= 65,536 scenarios, else 4 (auto_sub_batches)")
     ap.add_argument("--qp-tol", type=float, default=1e-10,
                     help="IPM stopping tolerance of the QPs (default 1e-10; 1e-8 = Clarabel's default, which "
                          "the reference runs with)")
@@ -398,6 +408,8 @@ def main():
     n = args.n
     total = args.total_batch
     B = args.batch if total is None else strong_shard(rank, world, total)[1]
+    if args.sub_batches is None:
+        args.sub_batches = min(auto_sub_batches(B), max(B, 1))
     if args.selftest:
         eng = _SelftestEngine(n, B, rank)
     else:
@@ -462,19 +474,22 @@ def main():
                                     "ipm_lane_utilisation": w["ipm_iters"] / max(w["slot_ipm_iters"], 1),
                                     "admm_slot_utilisation": w["qp_solves"] / n / max(w["wave_admm_iters"], 1)}
             k_ms = w["kernel_ms"]
-    kernel_ms = k_ms / max(hl_steps, 1)
-    if args.sub_batches > 1:
-        # the sub-batches' kernels overlap on their streams: no per-launch span of k_cadmm exists, so the
-        # rate is taken over the whole step's device time (a lower bound on the k_cadmm rate)
-        kernel = f"k_cadmm + step kernels ({args.sub_batches} sub-batch streams, whole-step device time)"
+    # k_cadmm launches per HL step: one per sub-batch stream
+    launches = max(hl_steps, 1) * max(args.sub_batches, 1)
+    kernel_ms = k_ms / launches
+    # (with sub-batch streams: one k_cadmm launch per sub-batch and step, each timed by its own event pair on
+    # its stream; the roofline is per launch, launches_per_step says how many)
     flops_launch = model_flops(args.mode, n, k_ipm, k_row, work.get("refine_passes", 0),
-                               work.get("refine_corrections", 0)) / max(hl_steps, 1)
+                               work.get("refine_corrections", 0)) / launches
     achieved_tflops = flops_launch / max(kernel_ms * 1e-3, 1e-12) / 1e12
     if total is None:
         workload = f"C4: {args.mode} n={n}, forest env ({args.start} start), {B} closed-loop scenarios per GPU"
     else:
         workload = (f"C4: {args.mode} n={n}, forest env ({args.start} start), {total} closed-loop scenarios split "
                     f"over {world} GPU(s)")
+    if args.sub_batches > 1:
+        workload += f", {args.sub_batches} sub-batch streams per GPU"
+
     traffic, traffic_src = traffic_per_launch(kernel, workload)
     out = {
         "metric": "agent-QP solves/sec (node) + ms per control step, 6-quad C-ADMM, 1/2/4/8 GPU",
@@ -484,8 +499,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
-        "ms_per_step_p50": float(np.percentile(per_step, 50)),
-        "ms_per_step_p99": float(np.percentile(per_step, 99)),
+        # (sub-batch streams run their steps independently: no per-step marks, no percentiles)
+        "ms_per_step_p50": None if args.sub_batches > 1 else float(np.percentile(per_step, 50)),
+        "ms_per_step_p99": None if args.sub_batches > 1 else float(np.percentile(per_step, 99)),
         "higher_is_better": True,
         "scaling": "weak" if total is None else "strong",
         "vs_baseline": None,
@@ -506,6 +522,7 @@ def main():
         "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "kernel": kernel, "launch_ms": kernel_ms,
+                     "launches_per_step": max(args.sub_batches, 1),
                      "flops_per_launch": flops_launch, "flop_model": model_string(args.mode)},
     }
     # (the CPU restatement solves at the default 1e-10: no work-matched baseline at another --qp-tol)

@@ -1694,6 +1694,7 @@ struct dat_handle {
   // C-ADMM closed loop on sub-batches (dat_set_sub_batches): contiguous scenario ranges, each with its own
   // stream, so one sub-batch's kernels fill the drain tail and the short kernels of the others
   int nsub = 1;
+  std::vector<hipEvent_t> sub_ev;  // closed_loop_sub: k_cadmm start / end events per sub-batch and step
   hipStream_t sub_stream[DAT_MAX_SUB] = {};
   hipEvent_t sub_done[DAT_MAX_SUB] = {};
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
@@ -2042,6 +2043,7 @@ int dat_destroy(dat_handle* h) {
   }
   if (h->ev_start) (void)hipEventDestroy(h->ev_start);
   if (h->ev_end) (void)hipEventDestroy(h->ev_end);
+  for (hipEvent_t e : h->sub_ev) (void)hipEventDestroy(e);
   if (h->e0) (void)hipEventDestroy(h->e0);
   if (h->e1) (void)hipEventDestroy(h->e1);
   if (h->ek) (void)hipEventDestroy(h->ek);
@@ -2253,6 +2255,12 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
   };
   h->marks.clear();
   h->marks.push_back(now_ms());
+  // k_cadmm launch spans: a start / end event pair per sub-batch and step, on the sub-batch's stream
+  while (h->sub_ev.size() < 2 * (size_t)S * hl_steps) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    h->sub_ev.push_back(e);
+  }
   HIPCHK(hipEventRecord(h->ev_start, h->stream));
   for (int s = 1; s < S; ++s) HIPCHK(hipStreamWaitEvent(h->sub_stream[s], h->ev_start, 0));
   for (int k = 0; k < hl_steps; ++k) {
@@ -2264,8 +2272,11 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
       const int G = 64 / n;
       hipLaunchKernelGGL(k_env_class, dim3((Bs + G - 1) / G), dim3(64), 0, st, a);
       hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, st, Bs, (const int*)a.need, a.slist, a.scount);
+      const hipEvent_t* ev = h->sub_ev.data() + 2 * ((size_t)k * S + s);
+      HIPCHK(hipEventRecord(ev[0], st));
       hipLaunchKernelGGL(k_cadmm, dim3(std::min((Bs + a.G - 1) / a.G, h->persistent_blocks)), dim3(64),
                          cadmm_lds_bytes(n, a.G, h->nforest > 0 ? NCLS - 1 : 0), st, a);
+      HIPCHK(hipEventRecord(ev[1], st));
       launch_rollout(a, Bs, st, h->cfg.hl_every, h->cfg.dt, (const double*)a.fdes);
       HIPCHK(hipGetLastError());
     }
@@ -2278,9 +2289,14 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
   HIPCHK(hipEventSynchronize(h->ev_end));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, h->ev_start, h->ev_end));
-  // the whole run's device time (the sub-batches' kernels overlap: no per-kernel span)
+  // hl_ms: the whole run's device time (the sub-batches' kernels overlap); cadmm_ms: the sum of the
+  // k_cadmm launch spans (S launches per HL step: dat_get_kernel_ms / (hl_steps S) is one launch)
   h->hl_ms += ms;
-  h->cadmm_ms += ms;
+  for (size_t j = 0; j < (size_t)S * hl_steps; ++j) {
+    float mk = 0.f;
+    HIPCHK(hipEventElapsedTime(&mk, h->sub_ev[2 * j], h->sub_ev[2 * j + 1]));
+    h->cadmm_ms += mk;
+  }
   h->hl_steps += hl_steps;
   h->marks.push_back(now_ms());
   return 0;

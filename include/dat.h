@@ -174,7 +174,9 @@ int dat_synchronize(dat_handle* h);
 int dat_set_persistent_blocks(dat_handle* h, int blocks);
 /* Summed device time [ms] since the last counter reset of the main solver kernel of each control step:
  * k_cadmm (C-ADMM) or k_dd (DD; the per-scenario quasi-Newton setup k_dd_setup excluded), 0 for
- * centralized.  Both are persistent queue drains; dat_set_persistent_blocks caps their grid. */
+ * centralized.  Both are persistent queue drains; dat_set_persistent_blocks caps their grid.  A closed
+ * loop on S sub-batches (dat_set_sub_batches) launches k_cadmm S times per HL step, one per sub-batch:
+ * the sum then covers hl_steps x S launches. */
 int dat_get_kernel_ms(dat_handle* h, double* ms);
 /* Agent QPs since the last counter reset (every kernel) that stalled before the IPM tolerance (1e-10:
  * a numerical breakdown of the structured Newton solve at gaps ~1e-12, or the divergence stop) and

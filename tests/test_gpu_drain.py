@@ -189,7 +189,7 @@ def test_gpu_fused_steps_equal_separate_steps(mode, n, B, blocks):
     assert sep.work()["hl_steps"] == K
 
 
-@pytest.mark.parametrize("subs", [2, 3])
+@pytest.mark.parametrize("subs", [2, 3, 4])
 def test_gpu_closed_loop_sub_batches_bitwise(subs):
     """dat_set_sub_batches: the C4 closed loop (desired acceleration, env classes, class sort, C-ADMM drain,
     rollout) on 2 or 3 sub-batches, each on its own stream with no synchronisation between them, must
