@@ -161,3 +161,13 @@ def test_sharding_gather_uneven_gloo_world3(tmp_path):
     assert np.array_equal(rows[:, 1], [0, 0, 0, 0, 1, 1, 1, 2, 2, 2])
     np.testing.assert_array_equal(v[2 * total: 2 * total + 2], [10.0, 3.0])
     np.testing.assert_array_equal(v[2 * total + 2:], [4.0, 2.0])
+
+
+def test_auto_sub_batches_policy():
+    """C4 stream count per GPU: one stream for the full 65,536-scenario batch (the N = 1 headline), four for
+    the per-GPU batches of the 2-, 4- and 8-GPU strong splits of BASELINE configs[3]."""
+    from distributed_aerial_transportation_amd.sharding import shard_range
+
+    assert bench.auto_sub_batches(65536) == 1
+    for world in (2, 4, 8):
+        assert bench.auto_sub_batches(shard_range(0, world, 65536)[1]) == 4
