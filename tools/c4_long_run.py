@@ -25,6 +25,9 @@ sf, st, forests = bench.bench_states(n, B, 0, 1, 64, "path", None)
 eng = BatchedController("cadmm", n, B, scenarios.params_block(n))
 eng.set_forests(forests, sf)
 eng.set_state(st, np.zeros(B, dtype=np.int32))
+subs = int(os.environ.get("SUBS", "1"))  # sub-batch streams (dat_set_sub_batches); marks then hold start / end only
+if subs > 1:
+    eng.set_sub_batches(subs)
 rows = []
 for b0 in range(0, steps, block):
     eng.reset_counters()
@@ -47,5 +50,5 @@ for b0 in range(0, steps, block):
     print(json.dumps(row), flush=True)
 os.makedirs(os.path.dirname(out), exist_ok=True)
 with open(out, "w") as f:
-    json.dump({"workload": "C4: cadmm n=6, forest env (path start), 65536 closed-loop scenarios, 1 GPU",
-               "blocks": rows}, f, indent=1)
+    json.dump({"workload": "C4: cadmm n=6, forest env (path start), 65536 closed-loop scenarios, 1 GPU"
+               + (f", {subs} sub-batch streams" if subs > 1 else ""), "blocks": rows}, f, indent=1)
