@@ -437,6 +437,9 @@ def main():
     work = eng.work()
     qps, ipm, hl_steps, hl_ms = work["qp_solves"], work["ipm_iters"], work["hl_steps"], work["hl_kernel_ms"]
     row_it = work["ipm_row_iters"]
+    # per-class counters and the k_cadmm event time of the timed steps, read before the metrics step
+    # below (its launch is not part of the timed region)
+    class_w = [eng.class_work(k) for k in range(4)] if args.mode == "cadmm" else None
     # per-scenario metrics of the last step (all-gathered over ranks: the only collective)
     res = eng.control(None, None)
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
@@ -467,7 +470,7 @@ def main():
         # one persistent k_cadmm launch per control step drains the four env classes
         classes = {}
         for k in range(4):
-            w = eng.class_work(k)
+            w = class_w[k]
             classes[f"class{k}"] = {"qp_solves": w["qp_solves"], "ipm_iters": w["ipm_iters"],
                                     "mean_active_rows": w["ipm_row_iters"] / max(w["ipm_iters"], 1),
                                     # useful lane-iterations / lane-iterations the wavefronts ran
