@@ -330,7 +330,8 @@ __device__ EnvOut env_rows_coop(const double* prm, int n, const double* st, cons
 
 // Two wavefronts per SIMD (256 VGPRs, 104 B/lane of scratch for the sorted row slots): the build without
 // the bound (290 registers, no scratch, one wavefront per SIMD) measured slower, C4 A/B 3.58 / 3.61 ->
-// 3.70 / 3.80 ms per step (round 4).
+// 3.70 / 3.80 ms per step (round 4).  Three or four wavefronts per SIMD (168 / 128 VGPRs, the sorted row
+// slots spilled) measured 3.2-3.6x slower by kernel trace: 0.24 -> 0.77 / 0.87 ms (round 4).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_env_class(KArgs a) {
   __shared__ int nd[64], cl[64];
   __shared__ double md[64];
