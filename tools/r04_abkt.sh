@@ -17,7 +17,7 @@ for rep in $(seq 1 ${REPS:-2}); do
 import csv,sys
 for r in csv.DictReader(open('$d/run_kernel_stats.csv')):
     n=r['Name']
-    if any(k in n for k in ('k_env_class','k_cadmm','k_rollout','k_bucket')): print('   ', n.split('(')[0].split('::')[-1], round(float(r['AverageNs'])/1e3,1), 'us avg', round(float(r['MinNs'])/1e3,1), 'min')
+    if any(k in n for k in ('k_env_class','k_cadmm','k_rollout','k_bucket','k_dd')): print('   ', n.split('(')[0].split('::')[-1], round(float(r['AverageNs'])/1e3,1), 'us avg', round(float(r['MinNs'])/1e3,1), 'min')
 "
   done
 done
