@@ -360,7 +360,8 @@ class _SelftestEngine:
         from types import SimpleNamespace
 
         return SimpleNamespace(iters=np.full(self.batch, 1 + self.rank, dtype=np.int32),
-                               min_env_dist=np.full(self.batch, 1.0), collision=np.zeros(self.batch, dtype=bool))
+                               min_env_dist=np.full(self.batch, 1.0), collision=np.zeros(self.batch, dtype=bool),
+                               qp_status=np.zeros((self.batch, self.n), dtype=np.int32))
 
 
 def timed_steps(eng, steps: int, barrier):
@@ -442,7 +443,9 @@ def main():
     class_w = [eng.class_work(k) for k in range(4)] if args.mode == "cadmm" else None
     # per-scenario metrics of the last step (all-gathered over ranks: the only collective)
     res = eng.control(None, None)
-    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
+    # per scenario: outer iterations, min env distance, collision flag, agent QPs not OPTIMAL
+    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64),
+                              (np.asarray(res.qp_status) != 0).sum(axis=1).astype(np.float64)], 1)
     tot = np.array([qps, ipm, hl_ms, elapsed, row_it, work.get("inband_exits", 0), B,
                     work.get("inband_beyond_clarabel_tol", 0)], dtype=np.float64)
     if dist is not None:
@@ -518,6 +521,7 @@ def main():
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
                   "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
+                  "non_optimal_agent_qps_last_step": int(all_metrics[:, 3].sum()),
                   "hl_kernel_ms_per_step": launch_ms, "env_classes": classes,
                   # agent QPs accepted through the best in-band iterate, and those beyond Clarabel's
                   # 1e-8 tolerance (dat_get_inband_exits)
@@ -600,7 +604,9 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     w = eng.work()
     kms = eng.kernel_ms()  # k_cadmm / k_dd of the timed steps (before the metrics-only step below)
     res = eng.control(None, L.f64(accs[0]))  # metrics only (outside the timed region)
-    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64)], 1)
+    # per scenario: outer iterations, min env distance, collision flag, agent QPs not OPTIMAL
+    local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64),
+                              (np.asarray(res.qp_status) != 0).sum(axis=1).astype(np.float64)], 1)
     tot = np.array([w["qp_solves"], w["ipm_iters"], w["hl_kernel_ms"], elapsed, w["ipm_row_iters"]])
     if dist is not None:
         sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, f"cuda:{local}")
@@ -638,6 +644,7 @@ def qp_level(args, dist, rank: int, world: int, local: int):
                    "parallelism": f"scenario-sharded x{world}"},
         "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
                   "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
+                  "non_optimal_agent_qps_last_step": int(all_metrics[:, 3].sum()),
                   "kernel_ms_per_step": step_ms, "inband_exits": int(w.get("inband_exits", 0)),
                   "inband_beyond_clarabel_tol": int(w.get("inband_beyond_clarabel_tol", 0))},
         "roofline": {"bound": "fp64-valu", "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
