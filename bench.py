@@ -618,7 +618,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
         if dist is not None:
             dist.destroy_process_group()
         return
-    kernel = {"cadmm": "k_cadmm", "dd": "k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
+    # (the QP-level configs have no forest: the C-ADMM drain is the class-0 kernel k_cadmm0)
+    kernel = {"cadmm": "k_cadmm0", "dd": "k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
     step_ms = float(tot[2]) / max(w["hl_steps"], 1)
     launch_ms = kms / max(w["hl_steps"], 1) if args.mode != "centralized" else step_ms
     flops_launch = model_flops(args.mode, n, float(tot[1]), float(tot[4]), w.get("refine_passes", 0),

@@ -736,6 +736,12 @@ __global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm(KArgs a) {
   cadmm_drain<1>(a);
   cadmm_drain<0>(a);
 }
+// Without a forest every scenario is in env class 0 (k_env_class finds no tree): the class-0 drain in a
+// kernel of its own, with a 960 B/lane scratch frame instead of k_cadmm's 1,728 (same arithmetic).  C5
+// 84.2 / 84.1 -> 80.3 / 79.9 ms per step, C2 12.7 / 12.9 -> 12.0 / 12.1 (round 4, kernel-trace A/B).
+// With a forest one launch per class measured 2x slower on C4 (each class launch drains to its own
+// tail): k_cadmm keeps the four drains in one launch there.
+__global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm0(KArgs a) { cadmm_drain<0>(a); }
 
 // ------------------------------------------------------------------------------------------------
 // DD: quasi-Newton matrix inverse per scenario (one 64-lane block per scenario)
@@ -1803,6 +1809,14 @@ size_t dd_setup_lds(int n) {
   return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + dd_setup_hs(n) + N);
 }
 
+// the C-ADMM drain of one control step: k_cadmm (env classes 3, 2, 1, 0) with a forest, k_cadmm0 without
+void launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st) {
+  if (h->nforest > 0)
+    hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
+  else
+    hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
+}
+
 // ksteps > 1 (dat_control_steps): that many control steps fused into one drain, acc_seq ksteps x B x 6
 int launch_hl(dat_handle* h, int ksteps = 1, const double* acc_seq = nullptr) {
   KArgs a = kargs(h);
@@ -1820,8 +1834,7 @@ int launch_hl(dat_handle* h, int ksteps = 1, const double* acc_seq = nullptr) {
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
     const int Gc = a.G, cblocks = (B + Gc - 1) / Gc;
-    hipLaunchKernelGGL(k_cadmm, dim3(std::min(cblocks, h->persistent_blocks)), dim3(64),
-                       cadmm_lds_bytes(n, Gc, h->nforest > 0 ? NCLS - 1 : 0), h->stream, a);
+    launch_cadmm(h, a, std::min(cblocks, h->persistent_blocks), h->stream);
   } else if (h->cfg.mode == DAT_MODE_DD) {
     if (n > DD_REG_NMAX)  // [H | I] in LDS: beyond the default 64 KB dynamic LDS from n = 11 on
       HIPCHK(hipFuncSetAttribute((const void*)k_dd_setup<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2275,8 +2288,7 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
       hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, st, Bs, (const int*)a.need, a.slist, a.scount);
       const hipEvent_t* ev = h->sub_ev.data() + 2 * ((size_t)k * S + s);
       HIPCHK(hipEventRecord(ev[0], st));
-      hipLaunchKernelGGL(k_cadmm, dim3(std::min((Bs + a.G - 1) / a.G, h->persistent_blocks)), dim3(64),
-                         cadmm_lds_bytes(n, a.G, h->nforest > 0 ? NCLS - 1 : 0), st, a);
+      launch_cadmm(h, a, std::min((Bs + a.G - 1) / a.G, h->persistent_blocks), st);
       HIPCHK(hipEventRecord(ev[1], st));
       launch_rollout(a, Bs, st, h->cfg.hl_every, h->cfg.dt, (const double*)a.fdes);
       HIPCHK(hipGetLastError());
