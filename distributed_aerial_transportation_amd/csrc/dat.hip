@@ -112,10 +112,7 @@ __host__ __device__ inline size_t cadmm_area_doubles(int cls, int rmode) {
 // alone for classes ROWLDS_MIN_CLS .. 2; class 3 (13 slots) never.  Few row slots without aux slots
 // are cheaper in registers: an LDS row access costs an LDS round trip, which pays only once the rows
 // would otherwise spill.
-#ifndef DAT_ROWLDS_MIN_CLS
-#define DAT_ROWLDS_MIN_CLS 1
-#endif
-constexpr int ROWLDS_MIN_CLS = DAT_ROWLDS_MIN_CLS;
+constexpr int ROWLDS_MIN_CLS = 1;
 __host__ __device__ inline int cadmm_row_mode(int n, int G, int cls) {
   if (cls >= NCLS - 1) return 0;
   if (cadmm_auxm(cls) && cadmm_fixed_bytes(n, G) + sizeof(double) * cadmm_area_doubles(cls, 2) <= LDS_WAVE_BUDGET)
@@ -725,12 +722,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
 // instantiation of the IPM.  All wavefronts work on the same class at (nearly) the same time: the
 // unrolled IPM of one class is ~80-130 KB of code, and wavefronts of different classes sharing a
 // CU's instruction cache measured 16 % slower (proportional class starts: 12.9 vs 11.1 ms, C4 path).
-#ifdef DAT_CADMM_WPE  // development knob: register budget of k_cadmm (waves per SIMD)
-#define DAT_CADMM_ATTR __attribute__((amdgpu_waves_per_eu(DAT_CADMM_WPE)))
-#else
-#define DAT_CADMM_ATTR
-#endif
-__global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm(KArgs a) {
+__global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   cadmm_drain<3>(a);
   cadmm_drain<2>(a);
   cadmm_drain<1>(a);
@@ -741,7 +733,7 @@ __global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm(KArgs a) {
 // 84.2 / 84.1 -> 80.3 / 79.9 ms per step, C2 12.7 / 12.9 -> 12.0 / 12.1 (round 4, kernel-trace A/B).
 // With a forest one launch per class measured 2x slower on C4 (each class launch drains to its own
 // tail): k_cadmm keeps the four drains in one launch there.
-__global__ __launch_bounds__(64) DAT_CADMM_ATTR void k_cadmm0(KArgs a) { cadmm_drain<0>(a); }
+__global__ __launch_bounds__(64) void k_cadmm0(KArgs a) { cadmm_drain<0>(a); }
 
 // ------------------------------------------------------------------------------------------------
 // DD: quasi-Newton matrix inverse per scenario (one 64-lane block per scenario)
