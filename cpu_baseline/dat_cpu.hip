@@ -82,7 +82,7 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
       lane_cadmm_dynamic(P[i], prm, n, i, Rt_all, lam + i * N3, fb, rho);
       P[i].tuned = it == 0 || prev_it <= 3;  // as k_cadmm (tuned IPM start: first pass / warm regime)
       double y[1][3], w[6], best[best_size(1)];
-      IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(rows_needed(P[i].emask), PlainRef<QPShared>{&S}, EnvPlain{&E[i]},
+      IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(rows_needed(P[i].emask), PlainRef<QPShared>{&S}, EnvPlain{&E[i]},
                                                RtPtr{Rt_all + 9 * i}, P[i], feq + 3 * i, y, w, best, 50, 1e-10);
       ++*qp;
       *ipm += o.iters;

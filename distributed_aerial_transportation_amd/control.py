@@ -289,9 +289,11 @@ class BatchedController:
         L.check(self._lib.dat_get_inband_exits(self._h, ctypes.byref(ib), ctypes.byref(lo)))
         rp, rc = ctypes.c_longlong(), ctypes.c_longlong()
         L.check(self._lib.dat_get_refinement_counters(self._h, ctypes.byref(rp), ctypes.byref(rc)))
+        rr = ctypes.c_longlong()
+        L.check(self._lib.dat_get_robust_redos(self._h, ctypes.byref(rr)))
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
                 "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value,
-                "refine_passes": rp.value, "refine_corrections": rc.value}
+                "refine_passes": rp.value, "refine_corrections": rc.value, "robust_redos": rr.value}
 
     def agent_qp_ms(self) -> float:
         """Device time of the last solve_agent_qps launch (dat_get_agent_qp_ms)."""

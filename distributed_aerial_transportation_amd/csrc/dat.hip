@@ -90,7 +90,7 @@ __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_r
 // doubles rounded up to a 16-byte multiple: every LDS region starts 16-byte aligned (pair reads)
 __host__ __device__ constexpr size_t al2(size_t d) { return (d + 1) & ~(size_t)1; }
 // per-slot ints done / sid / wmx (G each), rounded to 16 bytes
-__host__ __device__ constexpr int slot_ints(int G) { return (3 * G + 3) & ~3; }
+__host__ __device__ constexpr int slot_ints(int G) { return (4 * G + 3) & ~3; }
 __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
   return sizeof(double) * (al2((size_t)G * 3 * n) + (size_t)G * RT_STRIDE * n) + sizeof(QPShared) * (size_t)G +
          sizeof(int) * (size_t)slot_ints(G);
@@ -138,6 +138,8 @@ struct CadmmLds {
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
+  int* flag;  // per slot: k_cadmm: an agent QP turned stiff (the step goes to k_cadmm_rob); k_cadmm_rob: stiff rows
+              // were used this step
 };
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int rmode) {
   CadmmLds L;
@@ -147,6 +149,7 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.done = (int*)(L.sh + G);
   L.sid = L.done + G;
   L.wmx = L.sid + G;
+  L.flag = L.wmx + G;
   L.rows = (double*)(L.done + slot_ints(G));
   L.red = L.rows;
   const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
@@ -420,6 +423,8 @@ __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int
       count[cl] = sz;
       count[NCLS + cl] = st;
       count[2 * NCLS + cl] = 0;  // queue head of the class (k_cadmm)
+      count[3 * NCLS + cl] = 0;  // robust list of the class (k_cadmm -> k_cadmm_rob) and its head
+      count[4 * NCLS + cl] = 0;
       st += sz;
     }
   }
@@ -439,7 +444,12 @@ struct WaveCounters {
 // the start of the next ADMM pass, so a wavefront no longer idles until its slowest scenario of a
 // fixed group stops (SIMD occupancy: dat_get_class_occupancy).  A scenario's arithmetic does not
 // depend on which slot or wavefront runs it.
-template <int CLS>
+// RB = false (k_cadmm): the fast solver; a scenario one of whose agent QPs turns stiff (an active row's
+// barrier weight beyond IPM_STIFF_W, ipm_solve IPM_FAST_EXIT) stops at once and goes to its class's robust
+// list, and so does a scenario whose previous step needed the robust solver (rflag).  RB = true
+// (k_cadmm_rob, launched after k_cadmm): drains the robust lists, redoing each listed scenario's step
+// from the warm state k_cadmm saved when it took the scenario, with the robust solver (IPM_ROBUST).
+template <int CLS, bool RB>
 __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr bool ENV = CLS > 0;
   constexpr int NR = cadmm_nr(CLS);
@@ -450,8 +460,11 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
   const int lsc = ls < G ? ls : 0;
-  const int cnt = a.scount[CLS], first = a.scount[NCLS + CLS];
+  const int first = a.scount[NCLS + CLS];
+  const int cnt = RB ? a.scount[3 * NCLS + CLS] : a.scount[CLS];
   if (cnt == 0) return;
+  int* const qh = RB ? a.scount + 4 * NCLS + CLS : a.qhead + CLS;
+  const int* const ql = (RB ? a.rlist : a.slist) + first;
   const int rmode = cadmm_row_mode(n, G, CLS);  // wave-uniform
   CadmmLds L = cadmm_carve(smem, n, G, CLS, rmode);
   double* fb = L.fbar + lsc * N3;
@@ -481,10 +494,17 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     // ---- refill empty slots from the queue
     DAT_PHASE(11);
     if (lane < NT && i == 0 && L.sid[ls] == -1) {
-      const int q = atomicAdd(a.qhead + CLS, 1);
-      L.sid[ls] = q < cnt ? a.slist[first + q] : -2;  // -2: queue drained, slot retires
+      int s2;
+      for (;;) {
+        const int q = atomicAdd(qh, 1);
+        s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
+        if (RB || s2 < 0 || !a.rflag[s2]) break;
+        a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = s2;  // straight to k_cadmm_rob
+      }
+      L.sid[ls] = s2;
       L.done[ls] = 0;
       L.wmx[ls] = 0;
+      L.flag[ls] = 0;
     }
     __syncthreads();
     const int slot_sc = lane < NT ? L.sid[ls] : -2;
@@ -494,10 +514,17 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       prm = prm_of(a, sc);
       const double* st = a.state + (size_t)sc * a.S;
       make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
-      for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       lam = a.clam + ((size_t)sc * n + i) * N3;
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
+      if (!RB) {
+        // k_cadmm saves the lane's part of the warm state the passes update in place (its multipliers and
+        // its copy f^(i); the mean is written only when the scenario stops), to restore it if the step turns
+        // stiff and k_cadmm_rob redoes it
+        const size_t wo = ((size_t)sc * n + i) * N3;
+        for (int c = 0; c < N3; ++c) { a.bclam[wo + c] = lam[c]; a.bcf[wo + c] = myf[c]; }
+      }
+      for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       bst = a.best + ((size_t)sc * n + i) * best_size(1);
       iter = 0;
       prev_iter = a.iters[sc];  // the previous step's ADMM iterations (rewritten when the scenario stops)
@@ -540,20 +567,25 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       IPMOut o;
       DAT_PHASE(10);
       constexpr unsigned AUXM = cadmm_auxm(CLS);
+      constexpr int RM = RB ? IPM_ROBUST : IPM_FAST_EXIT;
+      using SHT = LdsRef<QPShared>;
+      using ERT = EnvLdsN<NE>;
       if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
         if (AUXM != 0 && rmode == 2)
-          o = ipm_solve<MODE_CADMM, 1, NR, LdsRef<QPShared>, EnvLdsN<NE>, RtLds, RowLds, AUXM>(
+          o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, AUXM, NoGrp, RM>(
               shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane});
         else if (CLS >= ROWLDS_MIN_CLS && rmode == 1)
-          o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                           a.qp_tol, RowLds{L.rows, lane});
+          o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, 0, NoGrp, RM>(
+              shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane});
         else
-          o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                           a.qp_tol);
+          o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowRegs, 0, NoGrp, RM>(
+              shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol);
       } else {
-        o = ipm_solve<MODE_CADMM, 1, NR>(shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
-                                         a.qp_tol);
+        o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowRegs, 0, NoGrp, RM>(
+            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol);
       }
+      // k_cadmm: turned stiff -- the scenario's step goes to k_cadmm_rob; k_cadmm_rob: stiff rows used
+      if (RB ? o.stiff != 0 : o.why == 7) L.flag[ls] = 1;
       DAT_PHASE(9);
       wc.ipm += o.iters;
       wc.inband += o.inband;
@@ -650,7 +682,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           res = fmax(res, fmax(sF, sM));
         }
       }
-      bool stop = (res < a.res_tol) || (iter > a.max_iter);
+      bool stop = (res < a.res_tol) || (iter > a.max_iter) || (!RB && L.flag[ls]);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
       L.done[ls] = stop ? 1 : 0;
     }
@@ -658,8 +690,21 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       if (!L.done[ls]) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
+      } else if (!RB && L.flag[ls]) {
+        // turned stiff: restore the warm state; k_cadmm_rob redoes the step
+        const size_t wo = ((size_t)sc * n + i) * N3;
+        for (int c = 0; c < N3; ++c) { lam[c] = a.bclam[wo + c]; myf[c] = a.bcf[wo + c]; }
+        if (i == 0) {
+          a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = sc;
+          a.rflag[sc] = 1;
+          L.sid[ls] = -1;
+        }
       } else {
         // the scenario stopped: write its outputs and free the slot
+        if (RB && i == 0) {
+          a.rflag[sc] = L.flag[ls];  // the next step goes straight to k_cadmm_rob only if this one needed it
+          atomicAdd(a.counters + CNT_ROB, 1ull);
+        }
         for (int c = 0; c < 3; ++c) {
           a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
           a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
@@ -723,17 +768,27 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
 // unrolled IPM of one class is ~80-130 KB of code, and wavefronts of different classes sharing a
 // CU's instruction cache measured 16 % slower (proportional class starts: 12.9 vs 11.1 ms, C4 path).
 __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
-  cadmm_drain<3>(a);
-  cadmm_drain<2>(a);
-  cadmm_drain<1>(a);
-  cadmm_drain<0>(a);
+  cadmm_drain<3, false>(a);
+  cadmm_drain<2, false>(a);
+  cadmm_drain<1, false>(a);
+  cadmm_drain<0, false>(a);
+}
+// The steps k_cadmm handed over (an agent QP turned stiff), redone with the robust solver: a kernel of its own,
+// because the robust solver compiled into k_cadmm cost the fast path 36-60 % (register allocation, C4 A/B).
+// Launched after every k_cadmm; without a listed scenario its blocks return at once.
+__global__ __launch_bounds__(64) void k_cadmm_rob(KArgs a) {
+  cadmm_drain<3, true>(a);
+  cadmm_drain<2, true>(a);
+  cadmm_drain<1, true>(a);
+  cadmm_drain<0, true>(a);
 }
 // Without a forest every scenario is in env class 0 (k_env_class finds no tree): the class-0 drain in a
 // kernel of its own, with a 960 B/lane scratch frame instead of k_cadmm's 1,728 (same arithmetic).  C5
 // 84.2 / 84.1 -> 80.3 / 79.9 ms per step, C2 12.7 / 12.9 -> 12.0 / 12.1 (round 4, kernel-trace A/B).
 // With a forest one launch per class measured 2x slower on C4 (each class launch drains to its own
 // tail): k_cadmm keeps the four drains in one launch there.
-__global__ __launch_bounds__(64) void k_cadmm0(KArgs a) { cadmm_drain<0>(a); }
+__global__ __launch_bounds__(64) void k_cadmm0(KArgs a) { cadmm_drain<0, false>(a); }
+__global__ __launch_bounds__(64) void k_cadmm0_rob(KArgs a) { cadmm_drain<0, true>(a); }
 
 // ------------------------------------------------------------------------------------------------
 // DD: quasi-Newton matrix inverse per scenario (one 64-lane block per scenario)
@@ -1498,6 +1553,7 @@ __global__ void k_warm(KArgs a) {
         a.clam[((size_t)sc * n + i) * N3 + c] = 0.0;
       }
     for (int c = 0; c < N3; ++c) a.cfbar[(size_t)sc * N3 + c] = feq[c];
+    if (a.rflag) a.rflag[sc] = 0;
   }
   if (a.dlamF) {
     double s3[3] = {0, 0, 0};
@@ -1617,7 +1673,7 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
   double* bst = q.best + (size_t)k * best_size(1);
   IPMOut o = dd ? ipm_solve_rows<MODE_DD, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                              a.qp_tol)
-                : ipm_solve_rows<MODE_CADMM, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
+                : ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
                                                 IPM_MAX_ITER, a.qp_tol);
   if (dd) {
     double* xo = q.x + (size_t)k * 9;
@@ -1672,6 +1728,8 @@ struct dat_handle {
   double* mountain = nullptr;
   int nforest = 0;
   double *cf = nullptr, *cfbar = nullptr, *clam = nullptr;
+  double *bcf = nullptr, *bclam = nullptr;  // C-ADMM: warm state saved by k_cadmm (restored for k_cadmm_rob)
+  int *rlist = nullptr, *rflag = nullptr;                      // C-ADMM: robust lists, per-scenario routing flag
   double *dlamF = nullptr, *dlamM = nullptr, *dprev = nullptr, *dHinv = nullptr;
   double* pf = nullptr;
   double* best = nullptr;
@@ -1786,6 +1844,10 @@ KArgs kargs(dat_handle* h) {
   a.slist = h->slist;
   a.scount = h->scount;
   a.qhead = h->scount ? h->scount + 2 * NCLS : nullptr;
+  a.rlist = h->rlist;
+  a.rflag = h->rflag;
+  a.bcf = h->bcf;
+  a.bclam = h->bclam;
   a.ll_kind = h->ll_kind;
   return a;
 }
@@ -1802,11 +1864,17 @@ size_t dd_setup_lds(int n) {
 }
 
 // the C-ADMM drain of one control step: k_cadmm (env classes 3, 2, 1, 0) with a forest, k_cadmm0 without
+// k_cadmm_rob: blocks of the robust redo (the listed scenarios are few: stalls next to trees)
+constexpr int ROB_BLOCKS = 256;
 void launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st) {
-  if (h->nforest > 0)
+  const int rblocks = std::min(blocks, ROB_BLOCKS);
+  if (h->nforest > 0) {
     hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
-  else
+    hipLaunchKernelGGL(k_cadmm_rob, dim3(rblocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
+  } else {
     hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
+    hipLaunchKernelGGL(k_cadmm0_rob, dim3(rblocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
+  }
 }
 
 // ksteps > 1 (dat_control_steps): that many control steps fused into one drain, acc_seq ksteps x B x 6
@@ -1885,7 +1953,11 @@ KArgs sub_kargs(dat_handle* h, int off, int Bs, int s) {
   a.need += o;
   a.ipmx += o;
   a.slist += o;
-  a.scount = h->scount + 3 * NCLS * s;
+  a.rlist += o;
+  a.rflag += o;
+  a.bcf += o * n * N3;
+  a.bclam += o * n * N3;
+  a.scount = h->scount + SCOUNT_INTS * s;
   a.qhead = a.scount + 2 * NCLS;
   a.erows += (size_t)4 * DAT_NENV * n * o;
   a.emask += o * n;
@@ -2002,15 +2074,19 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->erows, (size_t)B * n * DAT_NENV * 4);
     rc |= dalloc(h, &h->emask, (size_t)B * n);
     rc |= dalloc(h, &h->slist, B);
-    rc |= dalloc(h, &h->scount, 3 * NCLS * DAT_MAX_SUB);  // one class table per sub-batch
+    rc |= dalloc(h, &h->scount, SCOUNT_INTS * DAT_MAX_SUB);  // one class table per sub-batch
     rc |= dalloc(h, &h->cf, B * n * N3);
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
+    rc |= dalloc(h, &h->bcf, B * n * N3);
+    rc |= dalloc(h, &h->bclam, B * n * N3);
+    rc |= dalloc(h, &h->rlist, B);
+    rc |= dalloc(h, &h->rflag, B);
   } else if (c.mode == DAT_MODE_DD) {
     rc |= dalloc(h, &h->need, B);
     rc |= dalloc(h, &h->ipmx, B);
     rc |= dalloc(h, &h->slist, B);
-    rc |= dalloc(h, &h->scount, 3 * NCLS);
+    rc |= dalloc(h, &h->scount, SCOUNT_INTS);
     rc |= dalloc(h, &h->dlamF, B * N3);
     rc |= dalloc(h, &h->dlamM, B * N3);
     rc |= dalloc(h, &h->dprev, B * n * 9);
@@ -2597,6 +2673,16 @@ int dat_get_kernel_ms(dat_handle* h, double* ms) {
 int dat_get_agent_qp_ms(dat_handle* h, double* ms) {
   if (!h || !ms) return fail("dat_get_agent_qp_ms: null argument");
   *ms = h->agent_qp_ms;
+  return 0;
+}
+
+int dat_get_robust_redos(dat_handle* h, long long* redos) {
+  if (!h) return fail("dat_get_robust_redos: null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c = 0;
+  HIPCHK(hipMemcpyAsync(&c, h->counters + CNT_ROB, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (redos) *redos = (long long)c;
   return 0;
 }
 

@@ -207,6 +207,75 @@ DAT_HD bool inv3_spd(const double* D, double* O) {
   return true;
 }
 
+// Square-root factor of D = kappa I + Gs'Gs for a 9 x 3 block Gs (columns gc[c]): Householder QR of the
+// stacked 12 x 3 matrix [sqrt(kappa) I; Gs], D = R'R.  Forming D itself cancels catastrophically once an
+// active cone makes Gs stiff: with |Gs| ~ 1e7-1e12 the entries of D carry absolute rounding errors
+// eps |Gs|^2 >> kappa, so the compliant directions of D (and of D^-1, kept as an explicit matrix) are lost
+// and the corrector's iterative refinement diverges.  QR is column-wise backward stable: the error it makes
+// in the compliant directions is ~eps |Gs| instead of eps |Gs|^2.  Packed output (sp3 layout, upper):
+// R[sp3(r, c)] = R_rc for r < c, R[sp3(j, j)] = 1 / R_jj.  Returns false on a non-finite or singular factor.
+DAT_HD bool qr_cone(double kappa, const double gc[3][9], double* R) {
+  const double sk = sqrt(kappa);
+  double A[3][12];  // A[c][i]: column c, row i
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) A[c][i] = (i == c) ? sk : 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) A[c][3 + i] = gc[c][i];
+  }
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    double nx = 0.0;
+#pragma unroll
+    for (int i = j; i < 12; ++i) nx += A[j][i] * A[j][i];
+    nx = sqrt(nx);
+    const double al = A[j][j] >= 0.0 ? -nx : nx;  // R_jj = al; v = x - al e_j
+    const double v0 = A[j][j] - al;
+    const double vv = nx * (nx + fabs(A[j][j]));  // v'v / 2
+    ok = ok && (vv > 0.0) && (fabs(al) < 1e300);
+    const double ivv = frcp(vv);
+#pragma unroll
+    for (int c = j + 1; c < 3; ++c) {
+      double s = v0 * A[c][j];
+#pragma unroll
+      for (int i = j + 1; i < 12; ++i) s += A[j][i] * A[c][i];
+      s *= ivv;
+      A[c][j] -= s * v0;
+#pragma unroll
+      for (int i = j + 1; i < 12; ++i) A[c][i] -= s * A[j][i];
+      R[sp3(j, c)] = A[c][j];
+    }
+    R[sp3(j, j)] = frcp(al);
+  }
+  return ok;
+}
+// o = D^-1 v = R^-1 R^-T v for the packed factor of qr_cone (o may alias v)
+DAT_HD void dsolve3(const double* R, const double* v, double* o) {
+  const double t0 = v[0] * R[0];
+  const double t1 = (v[1] - R[1] * t0) * R[3];
+  const double t2 = (v[2] - R[2] * t0 - R[4] * t1) * R[5];
+  const double o2 = t2 * R[5];
+  const double o1 = (t1 - R[4] * o2) * R[3];
+  o[0] = (t0 - R[1] * o1 - R[2] * o2) * R[0];
+  o[1] = o1;
+  o[2] = o2;
+}
+// explicit D^-1 (packed) from the factor of qr_cone: M = R^-1 (upper), D^-1 = M M'
+DAT_HD void dinv_explicit(const double* R, double* Di) {
+  const double m00 = R[0], m11 = R[3], m22 = R[5];
+  const double m01 = -R[1] * m11 * m00;
+  const double m12 = -R[4] * m22 * m11;
+  const double m02 = -(R[1] * m12 + R[2] * m22) * m00;
+  Di[0] = m00 * m00 + m01 * m01 + m02 * m02;
+  Di[1] = m01 * m11 + m02 * m12;
+  Di[2] = m02 * m22;
+  Di[3] = m11 * m11 + m12 * m12;
+  Di[4] = m12 * m22;
+  Di[5] = m22 * m22;
+}
+
 // 6x6 Cholesky of a packed SPD matrix into a packed lower factor (L[sp6(i,j)] = L_ij, i >= j);
 // diagonal entries hold 1 / L_jj.  Returns false if not SPD.
 DAT_HD bool chol6(const double* A, double* L) {

@@ -38,7 +38,13 @@ constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, 
 constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
 // IPM refinement passes run and corrections applied (all kernels; the executed-flop model)
 constexpr int CNT_REF = CNT_INBAND + 2;
-constexpr int DAT_NCOUNTERS = CNT_REF + 2;
+// C-ADMM control steps of a scenario redone by k_cadmm_rob (an agent QP turned stiff in k_cadmm)
+constexpr int CNT_ROB = CNT_REF + 2;
+constexpr int DAT_NCOUNTERS = CNT_ROB + 1;
+// class table of the C-ADMM / DD queues (k_bucket), per sub-batch: [0, NCLS) class sizes, [NCLS, 2 NCLS) class
+// starts in slist, [2 NCLS, 3 NCLS) queue heads; C-ADMM robust redo: [3 NCLS, 4 NCLS) sizes of the classes'
+// robust lists (rlist, same class starts), [4 NCLS, 5 NCLS) their queue heads
+constexpr int SCOUNT_INTS = 5 * NCLS;
 constexpr double INBAND_CLARABEL = IPM_CLARABEL_TOL;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
 
@@ -76,6 +82,9 @@ struct KArgs {
   int* slist;                    // C-ADMM: scenario ids grouped by class, then by key (k_bucket)
   int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
   int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
+  int* rlist;                    // C-ADMM: scenarios whose step k_cadmm_rob redoes, by class (class starts as slist)
+  int* rflag;                    // C-ADMM: per scenario, its previous step needed the robust solver (route it there)
+  double *bcf, *bclam;           // C-ADMM: the warm state k_cadmm saves when it takes a scenario
   double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
                                  //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
   unsigned* emask;               // C-ADMM: [B n] env row mask of the step

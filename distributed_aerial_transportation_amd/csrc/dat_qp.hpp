@@ -191,8 +191,21 @@ struct QPLane {
 // row slots an IPM instantiation must cover for a lane whose env mask is emask
 DAT_HD int rows_needed(unsigned emask) { return NBASE + (emask ? 32 - __builtin_clz(emask) : 0); }
 
+// Stiff rows: a row slot whose barrier weight z/s exceeds IPM_STIFF_W is kept out of the normal-equation
+// matrix M and solved in augmented (quasi-definite) form, at most IPM_NSTIFF per solve (see ipm_attempt)
+constexpr double IPM_STIFF_W = 1e12;
+constexpr int IPM_NSTIFF = 4;
+
 // size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6)
-DAT_HD constexpr int best_size(int NB) { return 3 * NB + 18; }
+// plus, behind it, the stiff-row scratch of an iteration (ipm_attempt): per stiff row j a column
+// H abar_j = (dy (3 NB), dw (6), du (6)), the row (a (3), on-dwl flag, s / z), its right-hand side g and
+// dual direction dz (and a temporary); the Cholesky factor of the Schur complement (packed lower, reciprocal diagonal)
+DAT_HD constexpr int best_rec(int NB) { return 3 * NB + 18; }
+DAT_HD constexpr int stiff_col(int NB) { return 3 * NB + 12; }
+constexpr int STIFF_ROW = 8;  // a0 a1 a2 on_dwl e g dz tmp
+DAT_HD constexpr int best_size(int NB) {
+  return best_rec(NB) + IPM_NSTIFF * (stiff_col(NB) + STIFF_ROW) + IPM_NSTIFF * (IPM_NSTIFF + 1) / 2;
+}
 // Clarabel's own tolerance: an in-band exit whose merit is above it is one Clarabel would not certify
 constexpr double IPM_CLARABEL_TOL = 1e-8;
 
@@ -467,6 +480,8 @@ DAT_HD bool soc_scaling(const double* s, const double* z, SocScale& S) {
   S.eta = sqrt(sn * izn);
   S.ieta = frcp(S.eta);
   S.k1 = frcp(1.0 + S.w0);
+  S.w0 = S.w0; S.w1 = S.w1; S.w2 = S.w2; S.w3 = S.w3;
+  S.eta = S.eta; S.ieta = S.ieta; S.k1 = S.k1;
   return true;
 }
 // o = W v (inv = false) or W^-1 v (inv = true); W = eta H(w), W^-1 = H(Jw)/eta
@@ -581,7 +596,7 @@ struct RowMem {
 };
 // aux slots of ipm_solve (AUXM bits): SCAL the stopping-rule scales and best merits (4), RES the
 // iteration's residuals r_y and R_f (3 NB + 6), LAM the scaled point lambda = W z (9 NB), DINV the
-// cone blocks' D^-1 and 1 / d0 (7 NB)
+// cone blocks' QR factor of D (qr_cone) and 1 / d0 (7 NB)
 constexpr unsigned AUX_SCAL = 1, AUX_RES = 2, AUX_LAM = 4, AUX_DINV = 8;
 __host__ __device__ constexpr int ipm_aux_doubles(int NB, unsigned AUXM) {
   return ((AUXM & AUX_SCAL) ? 4 : 0) + ((AUXM & AUX_RES) ? 3 * NB + 6 : 0) + ((AUXM & AUX_LAM) ? 9 * NB : 0) +
@@ -693,6 +708,7 @@ struct IPMOut {
                   // 4 cone block D, 5 Cholesky of M, 6 Cholesky of N
   int refs;       // refinement passes run (residual evaluations of the linearised system)
   int corrs;      // refinement corrections applied (core solves)
+  int stiff;      // (robust instantiation) stiff rows were solved in augmented form in some iteration
   double pi[6];   // u-space gradient C u + cu - A' z_rows at the solution
   double u[6];
 };
@@ -710,7 +726,10 @@ struct IPMOut {
 // row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
-template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP>
+// ROB: the robust instantiation (stiff rows in augmented form, below).  SEXIT: the fast instantiation stops
+// (why = 7) as soon as a row turns stiff, so that its caller can redo the solve robustly (ipm_solve).
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB,
+          bool SEXIT>
 DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
                           int start) {
@@ -730,6 +749,7 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
   out.why = 0;
   out.refs = 0;
   out.corrs = 0;
+  out.stiff = 0;
   out.merit = 1e300;
 #pragma unroll
   for (int r = 0; r < 6; ++r) { out.pi[r] = 0.0; out.u[r] = 0.0; }
@@ -1163,6 +1183,8 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
       soc_apply(S2[k], zk[k] + 5, l2, false);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { LAM(k, 1 + j) = l1[j]; LAM(k, 5 + j) = l2[j]; }
+      ID0(k) = ID0(k);
+      LAM(k, 0) = LAM(k, 0);
     }
 #ifdef DAT_IPM_TRACE
     for (int k = 0; k < NB; ++k)
@@ -1194,7 +1216,8 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
       winv(k, t, g);
       GTz(g, o);
     };
-    // D_k = kappa I + Gs'Gs (packed) and its inverse
+    // D_k = kappa I + Gs'Gs through its QR square-root factor (qr_cone: forming D cancels once an active
+    // cone makes Gs stiff); DI holds the factor, applied by dsolve3
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       double gc[3][9];
@@ -1203,20 +1226,10 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         double e[3] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0};
         gs_mul(k, e, gc[c]);
       }
-      double D[6];
+      double Rd[6];
+      okc = okc && qr_cone(kap, gc, Rd);
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = r; c < 3; ++c) {
-          double s = (r == c) ? kap : 0.0;
-#pragma unroll
-          for (int j = 0; j < 9; ++j) s += gc[r][j] * gc[c][j];
-          D[sp3(r, c)] = s;
-        }
-      double Di[6];
-      okc = okc && inv3_spd(D, Di);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) DI(k, j) = Di[j];
+      for (int j = 0; j < 6; ++j) DI(k, j) = Rd[j];
     }
     if constexpr (GRP::on) okc = grp.min(okc ? 1.0 : 0.0) > 0.5;
     if (!okc) {
@@ -1229,6 +1242,21 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
     // every eigenvalue >= 1 however large active rows make M, so the factorisation stays well
     // conditioned without a pivoted nonsymmetric LU; only P (21 doubles) is kept for the solves.
     // DD: Lm alone (reciprocal diagonal, for chol6_solve).
+    // Stiff rows.  Near the solution an active row's barrier weight z/s grows without bound; inside a
+    // stalled ADMM loop (multipliers ~1e3-1e4, rows with tiny coefficients) it reaches 1e10-1e22.  Folded
+    // into M = C + A'(Z/S)A it wipes out C's digits, and the row's dual direction dz = zw - (z/s) a.du is
+    // a difference of huge terms.  So the first IPM_NSTIFF rows (slot order) whose weight exceeds
+    // IPM_STIFF_W stay out of M; their dual directions are unknowns of a small augmented system
+    //   a_l . lin(du) + (s_l / z_l) dz_l = g_l      (row primal + complementarity, no 1/s anywhere)
+    // solved by a Schur complement on the stiff rows: du = du0 + sum_l dz_l H abar_l, where du0 is the
+    // core solve without them and H abar_l a core solve with the row's u-space coefficient as bu (the
+    // columns, once per iteration, kept in the lane's scratch record behind `best`).  Without stiff rows
+    // (every well-scaled QP) nothing changes.
+    bool stiff_seen = false;
+    unsigned smask = 0u;  // stiff row slots (the rows' data: the scratch record behind `best`)
+    double* const hcol = best + best_rec(NB);                    // [j][dy (3 NB), dw (6), du (6)]
+    double* const srec = hcol + IPM_NSTIFF * stiff_col(NB);      // [j][a0 a1 a2 on_dwl e g dz tmp]
+    double* const sfac = srec + IPM_NSTIFF * STIFF_ROW;          // Cholesky factor of S
     double Lm[21];  // DD: Cholesky factor of M;  CADMM / CENT: P = Lm N^-1 Lm' (schur_P)
     {
       double Mm[21];
@@ -1239,14 +1267,30 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         for (int l = 0; l < NR; ++l) {
           double sl, zl;
           rst.sz(l, sl, zl);
-          const double wgt = zl * frcp(sl);
+          double wgt = zl * frcp(sl);
           DAT_STAT_W(act(l) * wgt);
-          double* X = l < NWROW ? Xw : Xv;
           double a3v[3];
           ra3(l, a3v);
+          if (SEXIT && act(l) > 0.0 && wgt > IPM_STIFF_W) stiff_seen = true;
+          if (ROB && act(l) > 0.0 && wgt > IPM_STIFF_W && __builtin_popcount(smask) < IPM_NSTIFF) {
+            double* r = srec + __builtin_popcount(smask) * STIFF_ROW;
+            r[0] = a3v[0]; r[1] = a3v[1]; r[2] = a3v[2];
+            r[3] = l < NWROW ? 1.0 : 0.0;
+            r[4] = sl * frcp(zl);
+            smask |= 1u << l;
+            wgt = 0.0;
+          }
+          double* X = l < NWROW ? Xw : Xv;
           const double a0 = a3v[0], a1 = a3v[1], a2 = a3v[2];
           X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
           X[3] += wgt * a1 * a1; X[4] += wgt * a1 * a2; X[5] += wgt * a2 * a2;
+        }
+        // the fast instantiation hands a stiff solve over to the robust one (ipm_solve)
+        if constexpr (SEXIT) {
+          if (stiff_seen) {
+            out.why = 7;
+            break;
+          }
         }
         // Av = [im I, Bv];  Av' Xv Av = [[im^2 Xv, im Xv Bv], [., Bv' Xv Bv]];  Aw = [0, JTi]
         const auto& S = sh.get();
@@ -1294,15 +1338,21 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = K[k] * irho;
           // K_{-i}/rho + U_i Dinv U_i' = K/rho + U_i (Dinv - I/rho) U_i'
-          double Dm[6] = {DI(0, 0) - irho, DI(0, 1), DI(0, 2), DI(0, 3) - irho, DI(0, 4), DI(0, 5) - irho};
+          double Rd[6], Dm[6];
+          dinv(0, Rd);
+          dinv_explicit(Rd, Dm);
+          Dm[0] -= irho;
+          Dm[3] -= irho;
+          Dm[5] -= irho;
           add_UDUt(T, rt.get(0), Dm, 1.0);
         } else {
 #pragma unroll
           for (int k = 0; k < 21; ++k) T[k] = 0.0;
 #pragma unroll
           for (int k = 0; k < NB; ++k) {
-            double Di[6];
-            dinv(k, Di);
+            double Rd[6], Di[6];
+            dinv(k, Rd);
+            dinv_explicit(Rd, Di);
             add_UDUt(T, rt.get(k), Di, 1.0);
           }
           if constexpr (GRP::on) {
@@ -1338,9 +1388,9 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           Ut_apply(rt.get(k), Rfr, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) v[c] = bk[k][c] + t[c];
-          double Di[6];
-          dinv(k, Di);
-          spmv3(Di, v, dyn[k]);
+          double Rd[6];
+          dinv(k, Rd);
+          dsolve3(Rd, v, dyn[k]);
         }
 #pragma unroll
         for (int r = 0; r < 6; ++r) dwn[r] = dun[r];
@@ -1359,9 +1409,9 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           if (has_bu) Ut_apply(rt.get(k), bu, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) bk2[k][c] = bk[k][c] + t[c];
-          double Di[6];
-          dinv(k, Di);
-          spmv3(Di, bk2[k], v);
+          double Rd[6];
+          dinv(k, Rd);
+          dsolve3(Rd, bk2[k], v);
           U_apply(rt.get(k), v, ut);
 #pragma unroll
           for (int r = 0; r < 6; ++r) yv[r] += ut[r];
@@ -1387,9 +1437,9 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           Ut_apply(rt.get(k), tau, t);
 #pragma unroll
           for (int c = 0; c < 3; ++c) v[c] = bk2[k][c] - t[c];
-          double Di[6];
-          dinv(k, Di);
-          spmv3(Di, v, dyn[k]);
+          double Rd[6];
+          dinv(k, Rd);
+          dsolve3(Rd, v, dyn[k]);
         }
         if (MODE == MODE_CADMM) {
           double kt[6];
@@ -1429,7 +1479,7 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
     // rc_l = s_l z_l + cadd_l (cadd = 0 for the predictor; the corrector's second-order term is
     // formed in place from the predictor's row direction ddva/ddwa and its zw).  Outputs: dy, dw,
     // du, scaled dz of the cones (dzs_k), lam \ rsk (lrs_k, so dss_k = -lrs_k - dzs_k) and zw
-    // (row dz is zw - (z/s) a.lin(du)).
+    // (row dz is zw - (z/s) a.lin(du); a stiff row's zw is its dz).
     double dy[NB][3], dwv[6], du[6], dzs_k[NB][9], lrs_k[NB][9];
     auto ZW = [&](int l) -> decltype(auto) { return rst.w(l); };
     // tks_k = W^-1 rz_k - lam \ rsk
@@ -1440,6 +1490,51 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
       for (int j = 0; j < 9; ++j) t[j] -= lrs_k[k][j];
     };
+    // stiff rows (see the M assembly): the columns H abar_j (core solves with the row's u-space
+    // coefficient as bu) and the Cholesky factor of S_ij = a_i . lin(H abar_j) + (s_i / z_i) delta_ij,
+    // formed by the predictor's newton call; everything through the lane's scratch record, in run-time
+    // loops over the stiff rows (well-scaled QPs never enter)
+    const int nst = __builtin_popcount(smask);
+    if (nst > 0) out.stiff = 1;
+    // a_j . lin(v) of stiff row j
+    auto srow = [&](int j, const double* v) -> double {
+      const double* r = srec + j * STIFF_ROW;
+      double dv2[3], dw2[3];
+      lin(v, dv2, dw2);
+      const double* x = r[3] != 0.0 ? dw2 : dv2;
+      return r[0] * x[0] + r[1] * x[1] + r[2] * x[2];
+    };
+    // stiff-row step: residuals r_j (in scratch at offset `ro` of each row record) of the stiff rows'
+    // equations are turned into dz = S^-1 r (in place), and (yy, ww, uu) += sum_j dz_j H abar_j
+    auto stiff_update = [&](int ro, double yy[NB][3], double* ww, double* uu) {
+#pragma unroll 1
+      for (int i = 0; i < nst; ++i) {
+        double t = srec[i * STIFF_ROW + ro];
+#pragma unroll 1
+        for (int k = 0; k < i; ++k) t -= sfac[i * (i + 1) / 2 + k] * srec[k * STIFF_ROW + ro];
+        srec[i * STIFF_ROW + ro] = t * sfac[i * (i + 1) / 2 + i];
+      }
+#pragma unroll 1
+      for (int i = nst - 1; i >= 0; --i) {
+        double t = srec[i * STIFF_ROW + ro];
+#pragma unroll 1
+        for (int k = i + 1; k < nst; ++k) t -= sfac[k * (k + 1) / 2 + i] * srec[k * STIFF_ROW + ro];
+        srec[i * STIFF_ROW + ro] = t * sfac[i * (i + 1) / 2 + i];
+      }
+#pragma unroll 1
+      for (int j = 0; j < nst; ++j) {
+        const double f = srec[j * STIFF_ROW + ro];
+        const double* h = hcol + j * stiff_col(NB);
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) yy[k][c] += f * h[3 * k + c];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) { ww[q] += f * h[3 * NB + q]; uu[q] += f * h[3 * NB + 6 + q]; }
+      }
+    };
+    // stiff row slot l <-> scratch index j (position among the stiff slots)
+    auto spos = [&](int l) -> int { return __builtin_popcount(smask & ((1u << l) - 1u)); };
     auto newton = [&](const double rsk[NB][9], bool corr, const double* ddva, const double* ddwa, double sigmu) {
       double bk[NB][3], bu[6];
 #pragma unroll
@@ -1458,6 +1553,7 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
         for (int c = 0; c < 3; ++c) bk[k][c] = -RK(k, c) - g3[c];
       }
+      // stiff rows: right-hand sides g of their equations go to the scratch record (their zw is 0 in bu)
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
         double sl, zl, al3[3], bl;
@@ -1465,19 +1561,80 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         rowld(l, al3, bl);
         const double is = frcp(sl);
         const double rzl = sl - (dot3x(l, al3, dv, dw) + bl);
+        const bool stf = (smask >> l) & 1u;
         double cadd = 0.0;
         if (corr) {
           const double a = dot3x(l, al3, ddva, ddwa);
-          cadd = act(l) * ((-rzl + a) * (ZW(l) - zl * is * a) - sigmu);
+          cadd = act(l) * ((-rzl + a) * (stf ? (double)ZW(l) : ZW(l) - zl * is * a) - sigmu);
         }
-        ZW(l) = (zl * rzl - (sl * zl + cadd)) * is;
+        if (__builtin_expect(stf, 0)) {
+          srec[spos(l) * STIFF_ROW + 5] = rzl - sl - cadd * frcp(zl);
+          ZW(l) = 0.0;
+        } else {
+          ZW(l) = (zl * rzl - (sl * zl + cadd)) * is;
+        }
       }
       rows_adj(ZW, bu);
+      if (__builtin_expect(!corr && nst > 0, 0)) {
+        // the predictor's call first solves for the iteration's stiff-row columns H abar_j (bk = 0,
+        // Rf = 0, bu = abar_j) and factors their Schur complement
+#pragma unroll 1
+        for (int j = 0; j < nst; ++j) {
+          double ab[6];
+          {
+            const double* r = srec + j * STIFF_ROW;
+            double gv[3] = {0, 0, 0}, gw[3] = {0, 0, 0};
+            double* g = r[3] != 0.0 ? gw : gv;
+            g[0] = r[0]; g[1] = r[1]; g[2] = r[2];
+            adj(gv, gw, ab);
+          }
+          double zb[NB][3], z6[6] = {0, 0, 0, 0, 0, 0}, cy[NB][3], cw[6], cu[6];
+#pragma unroll
+          for (int k = 0; k < NB; ++k) zb[k][0] = zb[k][1] = zb[k][2] = 0.0;
+          core(zb, z6, ab, true, false, cy, cw, cu);
+          double* h = hcol + j * stiff_col(NB);
+#pragma unroll
+          for (int k = 0; k < NB; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) h[3 * k + c] = cy[k][c];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) { h[3 * NB + q] = cw[q]; h[3 * NB + 6 + q] = cu[q]; }
+        }
+        // Cholesky of the symmetrised Schur complement S, column by column
+#pragma unroll 1
+        for (int j = 0; j < nst; ++j) {
+          double d = srow(j, hcol + j * stiff_col(NB) + 3 * NB + 6) + srec[j * STIFF_ROW + 4];
+#pragma unroll 1
+          for (int k = 0; k < j; ++k) d -= sfac[j * (j + 1) / 2 + k] * sfac[j * (j + 1) / 2 + k];
+          const double id = frcp(sqrt(fmax(d, 1e-300)));
+          sfac[j * (j + 1) / 2 + j] = id;
+#pragma unroll 1
+          for (int i = j + 1; i < nst; ++i) {
+            double t = 0.5 * (srow(i, hcol + j * stiff_col(NB) + 3 * NB + 6) +
+                              srow(j, hcol + i * stiff_col(NB) + 3 * NB + 6));
+#pragma unroll 1
+            for (int k = 0; k < j; ++k) t -= sfac[i * (i + 1) / 2 + k] * sfac[j * (j + 1) / 2 + k];
+            sfac[i * (i + 1) / 2 + j] = t * id;
+          }
+        }
+    }
       {
         double rfv[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r) rfv[r] = RF(r);
         core(bk, rfv, bu, true, false, dy, dwv, du);
+      }
+      // stiff rows' dual directions dz (scratch, and their zw slots)
+      auto stiff_store = [&]() {
+#pragma unroll
+        for (int l = 0; l < NR; ++l)
+          if (__builtin_expect((smask >> l) & 1u, 0)) ZW(l) = srec[spos(l) * STIFF_ROW + 6];
+      };
+      if (__builtin_expect(nst > 0, 0)) {
+#pragma unroll 1
+        for (int j = 0; j < nst; ++j) srec[j * STIFF_ROW + 6] = srec[j * STIFF_ROW + 5] - srow(j, du);
+        stiff_update(6, dy, dwv, du);
+        stiff_store();
       }
       // the affine (predictor) direction only sets the step length, sigma and the corrector's
       // second-order term: it is used unrefined; the corrector -- the step actually taken -- is refined
@@ -1510,7 +1667,8 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
             double sl, zl, a[3];
             rst.sz(l, sl, zl);
             ra3(l, a);
-            const double dzl = ZW(l) - zl * frcp(sl) * dot3x(l, a, ddv, ddw);
+            const bool stf = (smask >> l) & 1u;
+            const double dzl = stf ? (double)ZW(l) : ZW(l) - zl * frcp(sl) * dot3x(l, a, ddv, ddw);
             double* g = l < NWROW ? gw : gv;
             g[0] += dzl * a[0]; g[1] += dzl * a[1]; g[2] += dzl * a[2];
           }
@@ -1539,6 +1697,14 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 #pragma unroll
           for (int r = 0; r < 6; ++r) ef[r] = 0.0;
         }
+        // stiff rows' equations a_l . lin(du) + (s_l / z_l) dz_l = g_l: their residuals
+        double eq = 0.0;
+#pragma unroll 1
+        for (int j = 0; j < nst; ++j) {
+          double* r = srec + j * STIFF_ROW;
+          const double q = r[5] - srow(j, du) - r[4] * r[6];
+          eq = fmax(eq, fabs(q));
+        }
         {  // the linearised system is already solved to rounding: the correction would be noise
            // (stopping here: C4 A/B k_cadmm 11.0 ms with two passes per solve -> 8.9 ms, round 2)
           double en = 0.0, sc = 1.0;
@@ -1552,8 +1718,9 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           }
 #pragma unroll
           for (int r = 0; r < 6; ++r) { en = fmax(en, fabs(ef[r])); sc = fmax(sc, fabs(RF(r))); }
+          en = fmax(en, eq);
 #ifdef DAT_IPM_TRACE
-          printf("    ref %d en %.3e sc %.3e\n", ref, en, sc);
+          printf("    ref %d en %.3e sc %.3e stiff %d\n", ref, en, sc, nst);
 #endif
           if (en <= 1e-12 * sc) {
             DAT_STAT(2);
@@ -1564,6 +1731,18 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         }
         ++out.corrs;
         core(ek, ef, nullptr, false, true, dy, dwv, du);
+        if (__builtin_expect(nst > 0, 0)) {
+          // the stiff-row residuals of the corrected (du, dz), solved into a dz correction (tmp)
+#pragma unroll 1
+          for (int j = 0; j < nst; ++j) {
+            double* r = srec + j * STIFF_ROW;
+            r[7] = r[5] - srow(j, du) - r[4] * r[6];
+          }
+          stiff_update(7, dy, dwv, du);
+#pragma unroll 1
+          for (int j = 0; j < nst; ++j) srec[j * STIFF_ROW + 6] += srec[j * STIFF_ROW + 7];
+          stiff_store();
+        }
       }
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
@@ -1572,7 +1751,11 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
         gs_mul(k, dy[k], g9);
 #pragma unroll
         for (int j = 0; j < 9; ++j) dzs_k[k][j] = tks[j] + g9[j];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dy[k][c] = dy[k][c];
       }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) { dwv[r] = dwv[r]; du[r] = du[r]; }
     };
     // row directions of the current Newton solution
     // (s_l, z_l) of the row: sl, zl (one pair read by the caller)
@@ -1581,7 +1764,7 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
       rowld(l, al3, bl);
       const double a = dot3x(l, al3, ddv, ddw);
       ds = -(sl - (dot3x(l, al3, dv, dw) + bl)) + a;
-      dz = ZW(l) - zl * frcp(sl) * a;
+      dz = ((smask >> l) & 1u) ? (double)ZW(l) : ZW(l) - zl * frcp(sl) * a;
     };
     // step_len / gap_at / the update take the row-space image (ddv, ddw) = lin(du) of the current
     // direction, computed once per direction by the caller
@@ -1706,14 +1889,14 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
       rzk_of(k, rz);
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
-        sk[k][j] += alpha * (-rz[j] - g[j]);
-        zk[k][j] += alpha * dz[j];
+        sk[k][j] = sk[k][j] + alpha * (-rz[j] - g[j]);
+        zk[k][j] = zk[k][j] + alpha * dz[j];
       }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) y[k][c] += alpha * dy[k][c];
+      for (int c = 0; c < 3; ++c) y[k][c] = y[k][c] + alpha * dy[k][c];
     }
 #pragma unroll
-    for (int r = 0; r < 6; ++r) w[r] += alpha * dwv[r];
+    for (int r = 0; r < 6; ++r) w[r] = w[r] + alpha * dwv[r];
     {
 #pragma unroll
       for (int l = 0; l < NR; ++l) {
@@ -1755,57 +1938,98 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 // the conservative start: with consensus multipliers ~1e2-1e3 (the first, cold steps of C5 / C2, a
 // stalled ADMM loop) the tuned start's small duals and 0.999 step fraction can stall (full-size C5 on the
 // CPU replica, diag/c5_cpu.py: 153 of 29.2 M agent QPs, 2 of them beyond 1e-8; every one of them
-// converges from the conservative start in 7-16 iterations).  One code instance runs both attempts
-// (unroll 1), so the retry costs no code size; out.iters counts the iterations of both.
+// converges from the conservative start in 7-16 iterations).
+//
+// ROBUST selects the instantiation (the robust one carries the stiff-row machinery, which measured 36-60 %
+// of k_cadmm's time on the fast path when compiled into the same kernel, C4 A/B: so the C-ADMM control
+// step runs the fast solver in k_cadmm and redoes the step of a scenario whose solve turned stiff in a
+// kernel of its own, k_cadmm_rob):
+//   IPM_FAST        fast, stiff rows kept in M (DD, centralized: their QPs do not reach the regime)
+//   IPM_FAST_EXIT   fast, returning why = 7 as soon as a row turns stiff (k_cadmm)
+//   IPM_ROBUST      robust (k_cadmm_rob)
+//   IPM_FAST_REDO   fast, redone robustly from scratch when it turns stiff (single-QP surfaces, host builds:
+//                   the per-QP equivalent of the k_cadmm / k_cadmm_rob pair)
+enum { IPM_FAST = 0, IPM_FAST_EXIT = 1, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0,
-          class GRP = NoGrp>
+          class GRP = NoGrp, int ROBUST = IPM_FAST>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
                         GRP grp = GRP{}) {
-  // First start: tuned for the C-ADMM agent QPs of the warm closed loop (P.tuned), conservative otherwise.
-  // A tuned attempt that does not converge cleanly is redone from the conservative start (a tuned attempt
-  // that has not converged in 20 iterations is not converging: C4's tuned solves take 4.3 on average and
-  // at most ~10).  A conservative attempt accepted through an in-band iterate outside Clarabel's 1e-8
-  // (rounding-path accidents, ~1 agent QP in 10^7 on C5 and C1: the same QPs on the host build converge
-  // from either start) is redone from another start (C-ADMM: tuned; DD / centralized: the conservative
-  // start scaled by 10), whose result is taken.  (Not the attempts that end with no in-band iterate:
-  // they already ran to max_iter, and a second 50 iterations lengthened C1's slowest wavefront by 45 %.)  One call site
-  // and two ints of loop state: every ipm_attempt instantiation is inlined once (a save / compare /
-  // restore of the first result cost k_cadmm 4 % and k_cent 50 % in register pressure, round 4).
-  const int first = MODE == MODE_CADMM && P.tuned ? 1 : 0;
-  int start = first, second = 0, done = 0, done_refs = 0, done_corrs = 0;
-  IPMOut o;
+  if constexpr (ROBUST == IPM_FAST_REDO) {
+    const IPMOut f = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_EXIT>(sh, er, rt, P, y0, y, w, best,
+                                                                                      max_iter, tol, rw, grp);
+    if (f.why != 7) return f;
+    IPMOut r = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                              tol, rw, grp);
+    r.iters += f.iters;
+    r.refs += f.refs;
+    r.corrs += f.corrs;
+    return r;
+  } else {
+    constexpr bool ROB = ROBUST == IPM_ROBUST, SEXIT = ROBUST == IPM_FAST_EXIT;
+    // First start: tuned for the C-ADMM agent QPs of the warm closed loop (P.tuned), conservative otherwise.
+    // A tuned attempt that does not converge cleanly is redone from the conservative start (a tuned attempt
+    // that has not converged in 20 iterations is not converging: C4's tuned solves take 4.3 on average and
+    // at most ~10).  A conservative attempt accepted through an in-band iterate outside Clarabel's 1e-8
+    // (rounding-path accidents, ~1 agent QP in 10^7 on C5 and C1: the same QPs on the host build converge
+    // from either start) is redone from another start (C-ADMM: tuned; DD / centralized: the conservative
+    // start scaled by 10), whose result is taken unless it is worse than the first: then the first start
+    // is run once more (the attempts are deterministic, so that reproduces the first result; keeping it in
+    // registers instead cost k_cadmm 4 % and k_cent 50 % in register pressure, round 4).  (Not the attempts
+    // that end with no in-band iterate: they already ran to max_iter, and a second 50 iterations lengthened
+    // C1's slowest wavefront by 45 %.)  One code instance runs every attempt (unroll 1).
+    const int first = MODE == MODE_CADMM && P.tuned ? 1 : 0;
+    int start = first, trip = 0, done = 0, done_refs = 0, done_corrs = 0;
+    int rank0 = 0;  // first attempt: 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
+    double merit0 = 0.0;
+    auto rank_of = [](const IPMOut& r) { return r.status != ST_OPTIMAL ? 2 : r.inband ? 1 : 0; };
+    IPMOut o;
 #pragma unroll 1
-  for (;;) {
-    o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP>(sh, er, rt, P, y0, y, w, best,
-                                                             start == 1 && !second && max_iter > 20 ? 20 : max_iter,
-                                                             tol, rw, grp, start);
-    o.iters += done;
-    o.refs += done_refs;
-    o.corrs += done_corrs;
-    if (second || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
-    if (start == 1) {
-      if (o.why == 0 && !o.inband) break;
-      start = 0;
-    } else {
-      if (!(o.status == ST_OPTIMAL && o.inband && o.merit > IPM_CLARABEL_TOL)) break;
-      start = MODE == MODE_CADMM ? 1 : 2;
+    for (;;) {
+      // (the tuned start as the first attempt is capped at 20 iterations: see above)
+      o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, ROB, SEXIT>(
+          sh, er, rt, P, y0, y, w, best, start == 1 && trip != 1 && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
+          start);
+      o.iters += done;
+      o.refs += done_refs;
+      o.corrs += done_corrs;
+      if (SEXIT && o.why == 7) break;  // turned stiff: the caller redoes it robustly
+      if (trip == 2) break;
+      if (trip == 1) {
+        const int r1 = rank_of(o);
+        if (r1 < rank0 || (r1 == rank0 && (r1 != 1 || o.merit <= merit0))) break;
+        start = first;  // the second attempt is worse: redo the first
+      } else {
+        if (o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
+        if (start == 1) {
+          if (o.why == 0 && !o.inband) break;
+          start = 0;
+        } else {
+          if (!(o.status == ST_OPTIMAL && o.inband && o.merit > IPM_CLARABEL_TOL)) break;
+          start = MODE == MODE_CADMM ? 1 : 2;
+        }
+        rank0 = rank_of(o);
+        merit0 = o.merit;
+      }
+      ++trip;
+      done = o.iters;
+      done_refs = o.refs;
+      done_corrs = o.corrs;
     }
-    second = 1;
-    done = o.iters;
-    done_refs = o.refs;
-    done_corrs = o.corrs;
+    return o;
   }
-  return o;
 }
 
 // Solve with the smallest row-slot instantiation that covers every lane of the wavefront
 // (nr_wave: wave-uniform maximum of rows_needed over the lanes taking part).
-template <int MODE, int NB, class SH, class ER, class RT>
+template <int MODE, int NB, int ROBUST = IPM_FAST, class SH, class ER, class RT>
 DAT_HD IPMOut ipm_solve_rows(int nr_wave, const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
                              const double* y0, double y[NB][3], double w[6], double* best, int max_iter, double tol) {
-  if (nr_wave <= NBASE) return ipm_solve<MODE, NB, NBASE>(sh, er, rt, P, y0, y, w, best, max_iter, tol);
-  return ipm_solve<MODE, NB, DAT_MAXROW>(sh, er, rt, P, y0, y, w, best, max_iter, tol);
+  if (nr_wave <= NBASE)
+    return ipm_solve<MODE, NB, NBASE, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                             tol);
+  return ipm_solve<MODE, NB, DAT_MAXROW, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST>(sh, er, rt, P, y0, y, w, best,
+                                                                                max_iter, tol);
 }
 
 }  // namespace dat

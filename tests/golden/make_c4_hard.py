@@ -1,0 +1,94 @@
+"""Fixture ref_c4_hard.npz: C4 stall stretches (n = 6 C-ADMM in seeded forests), answered by the oracle
+(oracle/controllers.py CADMM, pinned to the reference's loop by tests/test_oracle_golden.py).
+
+The states are captured from the GPU's own C4 10 s loop (tools/c4_stall_states.py: the scenarios that stall
+longest, one HL step before their first stall).  From each, the reference's controller (the oracle in
+Clarabel's role) runs K HL steps: the ADMM loop stalls at max_iter (control/rqp_cadmm.py:631-675, 101
+passes) in every step after the first, the consensus multipliers grow (:627-629) and the agent QPs carry
+active rows and cones whose barrier weights reach 1e10-1e19 -- the regime where the round-4 solver accepted
+in-band iterates outside Clarabel's 1e-8 (profiles/r04_c4_10s_loop.md).
+
+Inside a stall some agent QPs are infeasible (the hold-previous branch of control/rqp_cadmm.py:496-499).
+Clarabel certifies infeasibility and cvxpy then reports "infeasible" (hold); the oracle's dense IPM has no
+infeasibility certificate and ends such solves at max_iter or in a numerical breakdown.  For a finite
+problem the fixture takes both as hold -- the oracle's NUMERICAL -> f_eq convention stands for the
+reference's exception branch (non-finite data), which cannot occur here.  Recorded at the oracle's QP
+tolerance (f_des) and at 1e-10 (f_des_1e10: the loop's own sensitivity to solver accuracy).
+
+    python tests/golden/make_c4_hard.py <c4_stall_states.npz> <j,j,...> <K>
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from distributed_aerial_transportation_amd.system import RQPState  # noqa: E402
+from oracle import controllers as oc  # noqa: E402
+from oracle import forest as of  # noqa: E402
+from oracle import model as om  # noqa: E402
+from oracle import scenarios as osc  # noqa: E402
+from oracle.ipm import NUMERICAL, OPTIMAL  # noqa: E402
+
+OUT = os.path.join(HERE, "ref_c4_hard.npz")
+
+
+def run(x0, seed, K, tol):
+    import oracle.controllers as occ
+
+    orig = occ.solve_qp
+    occ.solve_qp = lambda *a, **k: orig(*a, tol=tol, **k)
+    orig_agent = oc.CADMM.solve_agent
+
+    def solve_agent(self, i, s, acc, env, rho):
+        P, q, G, h, dims, A, b = om.build_qp("cadmm", self.p, self.c, s, acc, env, i=i, f_eq=self.f_eq,
+                                             lam=self.lam[:, :, i], rho=rho, f_mean=self.f_mean)
+        r = occ.solve_qp(P, q, G, h, dims, A, b)
+        self.qp_iters.append(r.iters)
+        if r.status == NUMERICAL and not all(np.all(np.isfinite(v)) for v in (P, q, G, h)):
+            self.prev_f[i] = self.f_eq.copy()
+        elif r.status == OPTIMAL:
+            self.prev_f[i] = r.x[9:].reshape((3, self.n), order="F")
+        return self.prev_f[i], r
+
+    oc.CADMM.solve_agent = solve_agent
+    try:
+        n = 6
+        p = osc.params(n)
+        np.random.seed(seed)
+        forest = of.Forest()
+        ctl = oc.CADMM(p, osc.col_radius(n), forest)
+        s = RQPState.unpack(x0, n)
+        st = om.State(s.R, s.w, s.xl, s.vl, s.Rl, s.wl, project=False)
+        F, I = [], []
+        for k in range(K):
+            acc, _, _ = oc.desired_acceleration_forest(st, forest)
+            f, stat = ctl.control(st, acc)
+            F.append(f.copy()), I.append(stat.iter)
+            print(tol, seed, k, stat.iter, flush=True)
+            for _ in range(10):
+                fl, M = om.low_level_control(p, st, f)
+                st.integrate(*om.forward_dynamics(p, st, fl, M), 1e-3)
+    finally:
+        occ.solve_qp = orig
+        oc.CADMM.solve_agent = orig_agent
+    return np.array(F), np.array(I, dtype=np.int16)
+
+
+def main():
+    src = np.load(sys.argv[1])
+    js = [int(a) for a in sys.argv[2].split(",")]
+    K = int(sys.argv[3])
+    x0 = np.stack([src["states"][j] for j in js])
+    seeds = np.array([int(src["scen_forest"][j]) for j in js], dtype=np.int32)
+    F, I, F10 = [], [], []
+    for x, seed in zip(x0, seeds):
+        f, it = run(x, int(seed), K, 1e-11)
+        f10, _ = run(x, int(seed), K, 1e-10)
+        F.append(f), I.append(it), F10.append(f10)
+    np.savez_compressed(OUT, x0=x0, forest_seed=seeds, f_des=np.array(F), iters=np.array(I), f_des_1e10=np.array(F10))
+
+
+if __name__ == "__main__":
+    main()

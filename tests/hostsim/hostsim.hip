@@ -72,6 +72,9 @@ void hs_last_diag(double* merit, int* inband, int* why) {
 int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                    const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
                    int tuned, double* f_out, int* iters, int* inband);
+// stiff exits of the fast solver since the last call (hs_qp_cadmm_ex: the redo count of IPM_FAST_REDO)
+long long g_stiff_redo = 0;
+long long hs_stiff_redos() { return g_stiff_redo; }
 int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                 const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
                 double* f_out, int* iters) {
@@ -98,9 +101,16 @@ int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc
   lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
   P.tuned = tuned;
   double y[1][3], w[6], best[best_size(1)];
-  IPMOut o = ipm_solve_rows<MODE_CADMM, 1>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
-                                           RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50,
-                                           HS_TOL);
+  // the GPU's C-ADMM step: the fast solver, redone robustly when it turns stiff (k_cadmm / k_cadmm_rob)
+  IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_EXIT>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+                                                          RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w,
+                                                          best, 50, HS_TOL);
+  if (o.why == 7) {
+    ++g_stiff_redo;
+    o = ipm_solve_rows<MODE_CADMM, 1, IPM_ROBUST>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+                                                  RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50,
+                                                  HS_TOL);
+  }
   *inband = o.inband ? 10 * o.why + 1 : 0;
   diag(o);
   for (int j = 0; j < n; ++j) {

@@ -175,3 +175,58 @@ def test_sm_closed_loop_matches_reference():
         if i % 50 == 49:
             ref = pack_state(unpack_flat(d["states"][i], 3))
             assert np.max(np.abs(x - ref)) < 1e-9, i
+
+
+def test_c4_stall_stretch_matches_oracle():
+    """The C4 stall stretches of ref_c4_hard.npz (tests/golden/make_c4_hard.py, n = 6 in seeded forests,
+    101-pass ADMM stalls from the second step on) with every agent QP answered by the host build of the
+    device solver as the GPU's C-ADMM step runs it (the fast solver, redone robustly when a row turns
+    stiff): ADMM iteration counts exact and f_des within max(1e-5, 5 x the oracle's own sensitivity) at
+    every step.  The first 12 steps of both stretches (the round-4 solver left the oracle by 2e-4 at steps
+    16-17 of the second; the GPU test runs all 20)."""
+    from distributed_aerial_transportation_amd import scenarios
+    from distributed_aerial_transportation_amd.system import RQPState, pack_state
+    from oracle import controllers as oc
+    from oracle import forest as of
+
+    d = load("ref_c4_hard.npz")
+    n, K = 6, 12
+    p = osc.params(n)
+    prm = scenarios.params_block(n)
+    for j in range(d["x0"].shape[0]):
+        np.random.seed(int(d["forest_seed"][j]))
+        forest = of.Forest()
+        s0 = RQPState.unpack(d["x0"][j], n)
+        st = om.State(s0.R, s0.w, s0.xl, s0.vl, s0.Rl, s0.wl, project=False)
+        ctl = oc.CADMM(p, osc.col_radius(n), forest)
+        tally = {"pass": 0, "tuned": 1, "loose": 0}
+
+        def solve(self, i, s_, acc, env, rho):
+            lam = self.lam[:, :, i].T.reshape(-1).copy()
+            fbar = self.f_mean.T.reshape(-1).copy()
+            tuned = tally["tuned"] if tally["pass"] == 0 else 0
+            f, status, _, inb = hs.qp_cadmm_ex(prm, n, pack_state(s_), np.concatenate(acc), env.lhs, env.rhs, i, lam,
+                                               fbar, rho, tuned=tuned)
+            tally["loose"] += bool(inb) and hs.last_diag()[0] > 1e-8
+            if status == 0:
+                self.prev_f[i] = f.reshape(n, 3).T.copy()
+            if i == n - 1:
+                tally["pass"] += 1
+            return self.prev_f[i], None
+
+        ctl.solve_agent = solve.__get__(ctl)
+        prev = 0
+        for k in range(K):
+            tally["pass"], tally["tuned"] = 0, 1 if prev <= 3 else 0
+            acc, _, _ = oc.desired_acceleration_forest(st, forest)
+            f, stat = ctl.control(st, acc)
+            prev = stat.iter
+            assert stat.iter == d["iters"][j, k], (j, k)
+            ref = d["f_des"][j, k]
+            scale = max(1.0, np.max(np.abs(ref)))
+            sens = np.max(np.abs(d["f_des_1e10"][j, k] - ref)) / scale
+            assert np.max(np.abs(f - ref)) / scale < max(1e-5, 5.0 * sens), (j, k)
+            for _ in range(10):
+                fl, M = om.low_level_control(p, st, f)
+                st.integrate(*om.forward_dynamics(p, st, fl, M), 1e-3)
+        assert tally["loose"] == 0, j
