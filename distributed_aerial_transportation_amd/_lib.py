@@ -179,6 +179,8 @@ def lib() -> ctypes.CDLL:
                            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
         L = ctypes.CDLL(path)
         for name, (res, args) in EXPORTS.items():
+            if path != LIB_PATH and not hasattr(L, name):
+                continue  # an older A/B build lacks a later export; the in-tree build must have them all
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

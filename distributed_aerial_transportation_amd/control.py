@@ -55,7 +55,7 @@ class StepResult:
     iters: np.ndarray           # (B,)
     qp_status: np.ndarray       # (B, n)
     min_env_dist: np.ndarray    # (B,)
-    collision: np.ndarray       # (B,) bool
+    collision: Optional[np.ndarray]  # (B,) bool (None: not computed, control_steps)
     err_seq: Optional[np.ndarray] = None  # (B, max_iter + 1), NaN padded
     gpu_ms: float = 0.0
 
@@ -211,7 +211,8 @@ class BatchedController:
 
     def control_steps(self, acc_seq: np.ndarray) -> StepResult:
         """dat_control_steps: acc_seq (K, B, 6) -> K fused control steps of every scenario from the resident
-        states (C-ADMM / DD without a forest); the result holds the last step's outputs."""
+        states (C-ADMM / DD without a forest); the result holds the last step's outputs.  The fused path
+        evaluates no environment rows: min_env_dist is NaN and collision None (not computed)."""
         acc_seq = L.f64(acc_seq)
         K = acc_seq.shape[0]
         assert acc_seq.shape[1:] == (self.batch, 6), acc_seq.shape
@@ -221,11 +222,12 @@ class BatchedController:
         L.check(self._lib.dat_control_steps(self._h, int(K), L.ptr(acc_seq), L.ptr(f), L.ptr(it, L.I),
                                             L.ptr(qs, L.I)))
         return StepResult(f.reshape(self.batch, self.n, 3).transpose(0, 2, 1).copy(), it, qs,
-                          np.zeros(self.batch), np.zeros(self.batch, dtype=bool))
+                          np.full(self.batch, np.nan), None)
 
     def step_marks(self) -> np.ndarray:
         """Host clock marks [ms] of the last closed_loop call (dat_get_step_marks): its start, then each
-        HL step's control-kernel completion."""
+        HL step's control-kernel completion.  With sub-batch streams (set_sub_batches > 1) only the run's
+        start and end: np.diff gives one whole-run time, not per-step times."""
         m = self._lib.dat_get_step_marks(self._h, None, 0)
         if m < 0:
             L.check(m)
@@ -290,7 +292,8 @@ class BatchedController:
         rp, rc = ctypes.c_longlong(), ctypes.c_longlong()
         L.check(self._lib.dat_get_refinement_counters(self._h, ctypes.byref(rp), ctypes.byref(rc)))
         rr = ctypes.c_longlong()
-        L.check(self._lib.dat_get_robust_redos(self._h, ctypes.byref(rr)))
+        if hasattr(self._lib, "dat_get_robust_redos"):  # absent only from an older A/B build (DAT_LIB_PATH)
+            L.check(self._lib.dat_get_robust_redos(self._h, ctypes.byref(rr)))
         return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
                 "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value,
                 "refine_passes": rp.value, "refine_corrections": rc.value, "robust_redos": rr.value}
@@ -428,18 +431,17 @@ class _PrimalSolver:
 class RQPCADMMPrimalSolver(_PrimalSolver):
     """control/rqp_cadmm.py:26-507: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) ->
     (f (3, n), solve_time, collision, min_env_dist).  Exception -> f_eq (:491-494); non-OPTIMAL ->
-    previous solution (:496-499).  Difference from the reference: cadmm_rho defaults to 1.0 (the
-    controller's rho0, control/rqp_cadmm.py:556-567) instead of 0 (:487).  The reference calls rho = 0 only
+    previous solution (:496-499).  cadmm_rho defaults to 0 as in the reference (:487), which calls rho = 0 only
     in its constructor's warm-up solve (:131-140), where the copies f_j, j != i, are not unique (that solve
-    only seeds Clarabel's warm start); an explicit rho <= 0 raises ValueError instead of silently solving
-    another QP."""
+    only seeds Clarabel's warm start): rho <= 0 -- the default included -- raises ValueError instead of
+    silently solving another QP."""
 
     _mode = L.MODE_CADMM
 
     def _set_warm_start(self) -> None:
         self.prev_f = self.f_eq.copy()
 
-    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 1.0, f_mean=None):
+    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 0.0, f_mean=None):
         n = self.n
         if not float(cadmm_rho) > 0.0:
             raise ValueError(f"cadmm_rho must be > 0 (got {cadmm_rho}): at rho = 0 the agent QP's copies f_j, "

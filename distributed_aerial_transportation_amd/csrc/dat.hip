@@ -138,7 +138,7 @@ struct CadmmLds {
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
-  int* flag;  // per slot: k_cadmm: an agent QP turned stiff (the step goes to k_cadmm_rob); k_cadmm_rob: stiff rows
+  int* flag;  // per slot: k_cadmm: lanes whose solve was not clean (to k_cadmm_rob); k_cadmm_rob: redone robustly
               // were used this step
 };
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int rmode) {
@@ -444,11 +444,13 @@ struct WaveCounters {
 // the start of the next ADMM pass, so a wavefront no longer idles until its slowest scenario of a
 // fixed group stops (SIMD occupancy: dat_get_class_occupancy).  A scenario's arithmetic does not
 // depend on which slot or wavefront runs it.
-// RB = false (k_cadmm): the fast solver; a scenario one of whose agent QPs turns stiff (an active row's
-// barrier weight beyond IPM_STIFF_W, ipm_solve IPM_FAST_EXIT) stops at once and goes to its class's robust
-// list, and so does a scenario whose previous step needed the robust solver (rflag).  RB = true
-// (k_cadmm_rob, launched after k_cadmm): drains the robust lists, redoing each listed scenario's step
-// from the warm state k_cadmm saved when it took the scenario, with the robust solver (IPM_ROBUST).
+// Every agent QP is solved as ipm_solve IPM_FAST_REDO defines it: the fast solver, redone by the robust one
+// when it does not end cleanly.  RB = false (k_cadmm) carries only the fast solver (IPM_FAST): a scenario one
+// of whose agent QPs does not end cleanly leaves at the end of that pass's solves with a resume record (rres)
+// and goes to its class's robust list, and so does a scenario whose previous step needed the robust solver
+// (rflag: routing only).  RB = true (k_cadmm_rob, launched after k_cadmm) drains the
+// robust lists with IPM_FAST_REDO, resuming each scenario in the pass it left (re-solving there only the
+// agent QPs handed over), so a scenario's arithmetic does not depend on which kernel ran which pass.
 template <int CLS, bool RB>
 __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr bool ENV = CLS > 0;
@@ -488,6 +490,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   double* bst = nullptr;
   int iter = 0, prev_iter = 0, qstat = ST_OPTIMAL;
   int kstep = 0;  // fused control steps (dat_control_steps): the slot scenario's current step
+  int rmask = -1;  // k_cadmm_rob: the lanes that solve in the current pass (a resumed pass: those handed over)
   double rho = a.rho0;
   WaveCounters wc;
   for (;;) {
@@ -499,11 +502,16 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         const int q = atomicAdd(qh, 1);
         s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
         if (RB || s2 < 0 || !a.rflag[s2]) break;
-        a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = s2;  // straight to k_cadmm_rob
+        int* const rr = a.rres + (size_t)s2 * RRES_INTS;  // straight to k_cadmm_rob, from the step's start
+        rr[RRES_KSTEP] = 0;
+        rr[RRES_PASS] = 0;
+        rr[RRES_WMX] = 0;
+        rr[RRES_LANES] = -1;
+        a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = s2;
       }
       L.sid[ls] = s2;
       L.done[ls] = 0;
-      L.wmx[ls] = 0;
+      L.wmx[ls] = RB && s2 >= 0 ? a.rres[(size_t)s2 * RRES_INTS + RRES_WMX] : 0;
       L.flag[ls] = 0;
     }
     __syncthreads();
@@ -517,21 +525,25 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       lam = a.clam + ((size_t)sc * n + i) * N3;
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
-      if (!RB) {
-        // k_cadmm saves the lane's part of the warm state the passes update in place (its multipliers and
-        // its copy f^(i); the mean is written only when the scenario stops), to restore it if the step turns
-        // stiff and k_cadmm_rob redoes it
-        const size_t wo = ((size_t)sc * n + i) * N3;
-        for (int c = 0; c < N3; ++c) { a.bclam[wo + c] = lam[c]; a.bcf[wo + c] = myf[c]; }
-      }
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
-      bst = a.best + ((size_t)sc * n + i) * best_size(1);
+      bst = a.best + ((size_t)sc * n + i) * (RB ? best_size(1) : best_rec(1));
       iter = 0;
       prev_iter = a.iters[sc];  // the previous step's ADMM iterations (rewritten when the scenario stops)
       qstat = ST_OPTIMAL;
       rho = a.rho0;
       kstep = 0;
-      if (i == 0) build_shared(S, prm, n, st, a.acc + (size_t)sc * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+      rmask = -1;
+      if (RB) {
+        // where k_cadmm left the scenario (its warm state -- multipliers, copies, the mean -- is in place)
+        const int* const rr = a.rres + (size_t)sc * RRES_INTS;
+        kstep = rr[RRES_KSTEP];
+        iter = rr[RRES_PASS];
+        rmask = rr[RRES_LANES];
+        for (int q = 0; q < iter; ++q) rho = fmin(rho * a.tau, a.rho_max);  // the pass's rho, as k_cadmm had it
+        qstat = a.qstatus[(size_t)sc * n + i];  // the pass's status of a lane not solved again
+      }
+      if (i == 0)
+        build_shared(S, prm, n, st, a.acc + ((size_t)kstep * a.B + sc) * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
     }
     if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
     DAT_PHASE(12);
@@ -557,9 +569,10 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     }
     // ---- one ADMM pass of every occupied slot
     DAT_PHASE(14);
-    const bool active = slot_sc >= 0;
+    bool active = slot_sc >= 0;
     int it_lane = 0;
-    if (active) {
+    bool hand = false;  // k_cadmm: this lane's solve was not clean; k_cadmm_rob: it was redone robustly
+    if (active && ((rmask >> i) & 1)) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho, RT_STRIDE);
       DAT_PHASE(15);
       P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
@@ -567,7 +580,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       IPMOut o;
       DAT_PHASE(10);
       constexpr unsigned AUXM = cadmm_auxm(CLS);
-      constexpr int RM = RB ? IPM_ROBUST : IPM_FAST_EXIT;
+      constexpr int RM = RB ? IPM_FAST_REDO : IPM_FAST;
       using SHT = LdsRef<QPShared>;
       using ERT = EnvLdsN<NE>;
       if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
@@ -584,8 +597,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowRegs, 0, NoGrp, RM>(
             shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol);
       }
-      // k_cadmm: turned stiff -- the scenario's step goes to k_cadmm_rob; k_cadmm_rob: stiff rows used
-      if (RB ? o.stiff != 0 : o.why == 7) L.flag[ls] = 1;
+      hand = RB ? o.stiff != 0 : ipm_unclean(o);
       DAT_PHASE(9);
       wc.ipm += o.iters;
       wc.inband += o.inband;
@@ -615,7 +627,29 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     wc.slot += wave_max(it_lane);
     ++wc.pass;
     if (active) atomicMax(&L.wmx[ls], it_lane);
+    rmask = -1;
+    // the slot's lanes whose solve k_cadmm hands over (a ballot: the block is one wavefront; an LDS flag set
+    // in the solve block cost k_cadmm ~65 % more scratch); k_cadmm_rob: the step redid a solve (routing)
+    const unsigned long long hb = __ballot(hand);
+    const int hmask = lane < NT ? (int)((hb >> (ls * n)) & ((1ull << n) - 1ull)) : 0;
+    if (RB && hand) L.flag[ls] = 1;
     __syncthreads();
+    if (!RB && active && hmask) {
+      // an agent QP of the pass was not clean: k_cadmm_rob resumes the scenario here (the mean of the pass's
+      // start, the statuses of the pass's other solves; multipliers and copies are in place)
+      for (int c = 0; c < 3; ++c) a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
+      a.qstatus[(size_t)sc * n + i] = qstat;
+      if (i == 0) {
+        int* const rr = a.rres + (size_t)sc * RRES_INTS;
+        rr[RRES_KSTEP] = kstep;
+        rr[RRES_PASS] = iter;
+        rr[RRES_WMX] = L.wmx[ls];
+        rr[RRES_LANES] = hmask;
+        a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = sc;
+        L.sid[ls] = -1;
+      }
+      active = false;
+    }
     if (active) {
       ++iter;
       rho = fmin(rho * a.tau, a.rho_max);
@@ -682,7 +716,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           res = fmax(res, fmax(sF, sM));
         }
       }
-      bool stop = (res < a.res_tol) || (iter > a.max_iter) || (!RB && L.flag[ls]);
+      bool stop = (res < a.res_tol) || (iter > a.max_iter);
       if (!stop && a.record_err && a.err) a.err[(size_t)sc * (a.max_iter + 1) + iter - 1] = res;
       L.done[ls] = stop ? 1 : 0;
     }
@@ -690,19 +724,10 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       if (!L.done[ls]) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
-      } else if (!RB && L.flag[ls]) {
-        // turned stiff: restore the warm state; k_cadmm_rob redoes the step
-        const size_t wo = ((size_t)sc * n + i) * N3;
-        for (int c = 0; c < N3; ++c) { lam[c] = a.bclam[wo + c]; myf[c] = a.bcf[wo + c]; }
-        if (i == 0) {
-          a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = sc;
-          a.rflag[sc] = 1;
-          L.sid[ls] = -1;
-        }
       } else {
         // the scenario stopped: write its outputs and free the slot
         if (RB && i == 0) {
-          a.rflag[sc] = L.flag[ls];  // the next step goes straight to k_cadmm_rob only if this one needed it
+          a.rflag[sc] = L.flag[ls] != 0;  // the next step goes straight to k_cadmm_rob only if this one needed it
           atomicAdd(a.counters + CNT_ROB, 1ull);
         }
         for (int c = 0; c < 3; ++c) {
@@ -726,6 +751,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
             build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
                          prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
             L.wmx[ls] = 0;
+            L.flag[ls] = 0;  // k_cadmm_rob: whether this step redoes a solve robustly (the routing of the next)
           }
         } else if (i == 0) {
           L.sid[ls] = -1;
@@ -773,7 +799,7 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   cadmm_drain<1, false>(a);
   cadmm_drain<0, false>(a);
 }
-// The steps k_cadmm handed over (an agent QP turned stiff), redone with the robust solver: a kernel of its own,
+// The steps k_cadmm handed over (an agent QP not clean), finished with the robust redo: a kernel of its own,
 // because the robust solver compiled into k_cadmm cost the fast path 36-60 % (register allocation, C4 A/B).
 // Launched after every k_cadmm; without a listed scenario its blocks return at once.
 __global__ __launch_bounds__(64) void k_cadmm_rob(KArgs a) {
@@ -1169,7 +1195,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       }
       for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
       for (int c = 0; c < 9; ++c) myX[c] = prev[c];  // the controller's current (f, F, M)
-      bst = a.best + ((size_t)sc * n + i) * best_size(1);
+      bst = a.best + ((size_t)sc * n + i) * best_rec(1);
       iter = 0;
       qstat = ST_OPTIMAL;
       kstep = 0;
@@ -1728,8 +1754,7 @@ struct dat_handle {
   double* mountain = nullptr;
   int nforest = 0;
   double *cf = nullptr, *cfbar = nullptr, *clam = nullptr;
-  double *bcf = nullptr, *bclam = nullptr;  // C-ADMM: warm state saved by k_cadmm (restored for k_cadmm_rob)
-  int *rlist = nullptr, *rflag = nullptr;                      // C-ADMM: robust lists, per-scenario routing flag
+  int *rlist = nullptr, *rflag = nullptr, *rres = nullptr;  // C-ADMM: robust lists, routing flags, resume records
   double *dlamF = nullptr, *dlamM = nullptr, *dprev = nullptr, *dHinv = nullptr;
   double* pf = nullptr;
   double* best = nullptr;
@@ -1846,8 +1871,7 @@ KArgs kargs(dat_handle* h) {
   a.qhead = h->scount ? h->scount + 2 * NCLS : nullptr;
   a.rlist = h->rlist;
   a.rflag = h->rflag;
-  a.bcf = h->bcf;
-  a.bclam = h->bclam;
+  a.rres = h->rres;
   a.ll_kind = h->ll_kind;
   return a;
 }
@@ -1955,8 +1979,7 @@ KArgs sub_kargs(dat_handle* h, int off, int Bs, int s) {
   a.slist += o;
   a.rlist += o;
   a.rflag += o;
-  a.bcf += o * n * N3;
-  a.bclam += o * n * N3;
+  a.rres += o * RRES_INTS;
   a.scount = h->scount + SCOUNT_INTS * s;
   a.qhead = a.scount + 2 * NCLS;
   a.erows += (size_t)4 * DAT_NENV * n * o;
@@ -2078,8 +2101,7 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->cf, B * n * N3);
     rc |= dalloc(h, &h->cfbar, B * N3);
     rc |= dalloc(h, &h->clam, B * n * N3);
-    rc |= dalloc(h, &h->bcf, B * n * N3);
-    rc |= dalloc(h, &h->bclam, B * n * N3);
+    rc |= dalloc(h, &h->rres, B * RRES_INTS);
     rc |= dalloc(h, &h->rlist, B);
     rc |= dalloc(h, &h->rflag, B);
   } else if (c.mode == DAT_MODE_DD) {

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(64) void k_cent(KArgs a) {
   nr = wave_max(nr);
   if (valid) {
     double y[1][3], w[6];
-    double* bst = a.best + ((size_t)sc * 16 + k) * best_size(1);
+    double* bst = a.best + ((size_t)sc * 16 + k) * best_rec(1);
     const double* y0 = prm + DAT_P_FEQ(n) + 3 * kk;
     const IPMOut o = nr <= NBASE ? cent_solve<W, NBASE>(a, L, g, lane, P, active, y0, y, w, bst)
                                  : cent_solve<W, DAT_MAXROW>(a, L, g, lane, P, active, y0, y, w, bst);

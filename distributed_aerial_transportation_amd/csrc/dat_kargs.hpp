@@ -45,6 +45,10 @@ constexpr int DAT_NCOUNTERS = CNT_ROB + 1;
 // starts in slist, [2 NCLS, 3 NCLS) queue heads; C-ADMM robust redo: [3 NCLS, 4 NCLS) sizes of the classes'
 // robust lists (rlist, same class starts), [4 NCLS, 5 NCLS) their queue heads
 constexpr int SCOUNT_INTS = 5 * NCLS;
+// Resume record of a scenario k_cadmm hands to k_cadmm_rob: the fused control step and the ADMM pass it
+// stopped in, the IPM-iteration maximum so far, and the mask of its agent lanes whose solve of that pass
+// turned stiff (the others' results of the pass stand; all lanes for a scenario routed at claim)
+constexpr int RRES_KSTEP = 0, RRES_PASS = 1, RRES_WMX = 2, RRES_LANES = 3, RRES_INTS = 4;
 constexpr double INBAND_CLARABEL = IPM_CLARABEL_TOL;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
 
@@ -84,7 +88,7 @@ struct KArgs {
   int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
   int* rlist;                    // C-ADMM: scenarios whose step k_cadmm_rob redoes, by class (class starts as slist)
   int* rflag;                    // C-ADMM: per scenario, its previous step needed the robust solver (route it there)
-  double *bcf, *bclam;           // C-ADMM: the warm state k_cadmm saves when it takes a scenario
+  int* rres;                     // C-ADMM: per listed scenario, where k_cadmm_rob resumes it (RRES_* fields)
   double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
                                  //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs
   unsigned* emask;               // C-ADMM: [B n] env row mask of the step

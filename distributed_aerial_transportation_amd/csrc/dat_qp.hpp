@@ -196,8 +196,9 @@ DAT_HD int rows_needed(unsigned emask) { return NBASE + (emask ? 32 - __builtin_
 constexpr double IPM_STIFF_W = 1e12;
 constexpr int IPM_NSTIFF = 4;
 
-// size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6)
-// plus, behind it, the stiff-row scratch of an iteration (ipm_attempt): per stiff row j a column
+// size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6) (best_rec: all a
+// non-robust instantiation touches, the stride k_cadmm, DD and centralized index with) plus, behind it, the
+// robust instantiation's stiff-row scratch of an iteration (ipm_attempt): per stiff row j a column
 // H abar_j = (dy (3 NB), dw (6), du (6)), the row (a (3), on-dwl flag, s / z), its right-hand side g and
 // dual direction dz (and a temporary); the Cholesky factor of the Schur complement (packed lower, reciprocal diagonal)
 DAT_HD constexpr int best_rec(int NB) { return 3 * NB + 18; }
@@ -708,7 +709,7 @@ struct IPMOut {
                   // 4 cone block D, 5 Cholesky of M, 6 Cholesky of N
   int refs;       // refinement passes run (residual evaluations of the linearised system)
   int corrs;      // refinement corrections applied (core solves)
-  int stiff;      // (robust instantiation) stiff rows were solved in augmented form in some iteration
+  int stiff;      // IPM_ROBUST: stiff rows solved in augmented form in some iteration; IPM_FAST_REDO: redone robustly
   double pi[6];   // u-space gradient C u + cu - A' z_rows at the solution
   double u[6];
 };
@@ -726,10 +727,8 @@ struct IPMOut {
 // row 0 . x + 1 >= 0 with z = 0, whose complementarity target is zeroed, so it never moves and
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
-// ROB: the robust instantiation (stiff rows in augmented form, below).  SEXIT: the fast instantiation stops
-// (why = 7) as soon as a row turns stiff, so that its caller can redo the solve robustly (ipm_solve).
-template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB,
-          bool SEXIT>
+// ROB: the robust instantiation (stiff rows in augmented form, below).
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB>
 DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
                           int start) {
@@ -1252,7 +1251,6 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
     // core solve without them and H abar_l a core solve with the row's u-space coefficient as bu (the
     // columns, once per iteration, kept in the lane's scratch record behind `best`).  Without stiff rows
     // (every well-scaled QP) nothing changes.
-    bool stiff_seen = false;
     unsigned smask = 0u;  // stiff row slots (the rows' data: the scratch record behind `best`)
     double* const hcol = best + best_rec(NB);                    // [j][dy (3 NB), dw (6), du (6)]
     double* const srec = hcol + IPM_NSTIFF * stiff_col(NB);      // [j][a0 a1 a2 on_dwl e g dz tmp]
@@ -1271,7 +1269,6 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           DAT_STAT_W(act(l) * wgt);
           double a3v[3];
           ra3(l, a3v);
-          if (SEXIT && act(l) > 0.0 && wgt > IPM_STIFF_W) stiff_seen = true;
           if (ROB && act(l) > 0.0 && wgt > IPM_STIFF_W && __builtin_popcount(smask) < IPM_NSTIFF) {
             double* r = srec + __builtin_popcount(smask) * STIFF_ROW;
             r[0] = a3v[0]; r[1] = a3v[1]; r[2] = a3v[2];
@@ -1284,13 +1281,6 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
           const double a0 = a3v[0], a1 = a3v[1], a2 = a3v[2];
           X[0] += wgt * a0 * a0; X[1] += wgt * a0 * a1; X[2] += wgt * a0 * a2;
           X[3] += wgt * a1 * a1; X[4] += wgt * a1 * a2; X[5] += wgt * a2 * a2;
-        }
-        // the fast instantiation hands a stiff solve over to the robust one (ipm_solve)
-        if constexpr (SEXIT) {
-          if (stiff_seen) {
-            out.why = 7;
-            break;
-          }
         }
         // Av = [im I, Bv];  Av' Xv Av = [[im^2 Xv, im Xv Bv], [., Bv' Xv Bv]];  Aw = [0, JTi]
         const auto& S = sh.get();
@@ -1940,33 +1930,56 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 // CPU replica, diag/c5_cpu.py: 153 of 29.2 M agent QPs, 2 of them beyond 1e-8; every one of them
 // converges from the conservative start in 7-16 iterations).
 //
-// ROBUST selects the instantiation (the robust one carries the stiff-row machinery, which measured 36-60 %
-// of k_cadmm's time on the fast path when compiled into the same kernel, C4 A/B: so the C-ADMM control
-// step runs the fast solver in k_cadmm and redoes the step of a scenario whose solve turned stiff in a
-// kernel of its own, k_cadmm_rob):
-//   IPM_FAST        fast, stiff rows kept in M (DD, centralized: their QPs do not reach the regime)
-//   IPM_FAST_EXIT   fast, returning why = 7 as soon as a row turns stiff (k_cadmm)
-//   IPM_ROBUST      robust (k_cadmm_rob)
-//   IPM_FAST_REDO   fast, redone robustly from scratch when it turns stiff (single-QP surfaces, host builds:
-//                   the per-QP equivalent of the k_cadmm / k_cadmm_rob pair)
-enum { IPM_FAST = 0, IPM_FAST_EXIT = 1, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
+// ROBUST selects the instantiation.  The robust one carries the stiff-row machinery, which cost k_cadmm's fast
+// path 36-60 % when compiled into the same kernel (register allocation, C4 A/B), and so does any test for stiff
+// rows inside the fast one (7-14 %): a solve is judged by its outcome instead.  A fast solve that does not
+// end cleanly -- not converged to tolerance (INACCURATE), or accepted through an in-band iterate -- is the
+// symptom of stiff rows (a stalled ADMM loop's agent QPs, barrier weights 1e10-1e19, whose Newton systems
+// lose the digits convergence needs) and is redone by the robust instantiation from scratch; the better of
+// the two outcomes is kept (ipm_rank).  A clean fast solve meets the tolerance on residuals evaluated from
+// the iterate itself, however its Newton systems were solved.
+//   IPM_FAST        fast (k_cadmm, which hands a scenario with an unclean solve to k_cadmm_rob; DD, centralized)
+//   IPM_ROBUST      robust
+//   IPM_FAST_REDO   the C-ADMM agent QP's definition: fast, redone robustly when not clean (k_cadmm_rob, the
+//                   single-QP surfaces, host builds)
+enum { IPM_FAST = 0, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
+// 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
+DAT_HD int ipm_rank(const IPMOut& r) { return r.status != ST_OPTIMAL ? 2 : r.inband ? 1 : 0; }
+// a fast solve k_cadmm hands over (IPM_FAST_REDO redoes it): in-band, or INACCURATE (not the solver-exception
+// branch, ST_FAILED: non-finite data)
+DAT_HD bool ipm_unclean(const IPMOut& r) {
+  return r.status == ST_INACCURATE || (r.status == ST_OPTIMAL && r.inband);
+}
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0,
           class GRP = NoGrp, int ROBUST = IPM_FAST>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
                         GRP grp = GRP{}) {
   if constexpr (ROBUST == IPM_FAST_REDO) {
-    const IPMOut f = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_EXIT>(sh, er, rt, P, y0, y, w, best,
-                                                                                      max_iter, tol, rw, grp);
-    if (f.why != 7) return f;
+    const IPMOut f = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST>(sh, er, rt, P, y0, y, w, best,
+                                                                                 max_iter, tol, rw, grp);
+    if (!ipm_unclean(f)) return f;
     IPMOut r = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
                                                                               tol, rw, grp);
+    const int rf = ipm_rank(f), rr = ipm_rank(r);
+    if (rr > rf || (rr == rf && rr == 1 && r.merit > f.merit)) {
+      // the robust outcome is worse: the fast solve once more (deterministic: it reproduces f; keeping f's
+      // iterate instead would hold another y, w, pi, u live across the robust solve)
+      const IPMOut g = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST>(sh, er, rt, P, y0, y, w, best,
+                                                                                   max_iter, tol, rw, grp);
+      const int ri = r.iters, rf2 = r.refs, rc = r.corrs;
+      r = g;
+      r.iters += ri;
+      r.refs += rf2;
+      r.corrs += rc;
+    }
     r.iters += f.iters;
     r.refs += f.refs;
     r.corrs += f.corrs;
+    r.stiff = 1;  // redone robustly
     return r;
   } else {
-    constexpr bool ROB = ROBUST == IPM_ROBUST, SEXIT = ROBUST == IPM_FAST_EXIT;
+    constexpr bool ROB = ROBUST == IPM_ROBUST;
     // First start: tuned for the C-ADMM agent QPs of the warm closed loop (P.tuned), conservative otherwise.
     // A tuned attempt that does not converge cleanly is redone from the conservative start (a tuned attempt
     // that has not converged in 20 iterations is not converging: C4's tuned solves take 4.3 on average and
@@ -1982,21 +1995,19 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     int start = first, trip = 0, done = 0, done_refs = 0, done_corrs = 0;
     int rank0 = 0;  // first attempt: 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
     double merit0 = 0.0;
-    auto rank_of = [](const IPMOut& r) { return r.status != ST_OPTIMAL ? 2 : r.inband ? 1 : 0; };
     IPMOut o;
 #pragma unroll 1
     for (;;) {
       // (the tuned start as the first attempt is capped at 20 iterations: see above)
-      o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, ROB, SEXIT>(
+      o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, ROB>(
           sh, er, rt, P, y0, y, w, best, start == 1 && trip != 1 && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
           start);
       o.iters += done;
       o.refs += done_refs;
       o.corrs += done_corrs;
-      if (SEXIT && o.why == 7) break;  // turned stiff: the caller redoes it robustly
       if (trip == 2) break;
       if (trip == 1) {
-        const int r1 = rank_of(o);
+        const int r1 = ipm_rank(o);
         if (r1 < rank0 || (r1 == rank0 && (r1 != 1 || o.merit <= merit0))) break;
         start = first;  // the second attempt is worse: redo the first
       } else {
@@ -2008,7 +2019,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           if (!(o.status == ST_OPTIMAL && o.inband && o.merit > IPM_CLARABEL_TOL)) break;
           start = MODE == MODE_CADMM ? 1 : 2;
         }
-        rank0 = rank_of(o);
+        rank0 = ipm_rank(o);
         merit0 = o.merit;
       }
       ++trip;

@@ -148,7 +148,9 @@ int dat_closed_loop(dat_handle* h, int hl_steps);
 int dat_set_sub_batches(dat_handle* h, int count);
 /* Host steady-clock marks (ms) of the last dat_closed_loop call: [0] its start (0.0), then the completion
  * of each HL step's control kernel; consecutive differences are per-step times of the back-to-back run.
- * Writes up to max_marks values; returns the number of marks (hl_steps + 1). */
+ * Writes up to max_marks values; returns the number of marks (hl_steps + 1).  With sub-batch streams
+ * (dat_set_sub_batches > 1) the steps of different sub-batches overlap: only the start and the end of the
+ * run are marked (2 marks), so consecutive differences give one whole-run time, not per-step times. */
 int dat_get_step_marks(dat_handle* h, double* marks_ms, int max_marks);
 
 /* ---- counters since the last reset: agent-QP solves, IPM iterations, IPM iterations x active

@@ -101,16 +101,11 @@ int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc
   lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
   P.tuned = tuned;
   double y[1][3], w[6], best[best_size(1)];
-  // the GPU's C-ADMM step: the fast solver, redone robustly when it turns stiff (k_cadmm / k_cadmm_rob)
-  IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_EXIT>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
+  // the GPU's C-ADMM agent QP (k_cadmm / k_cadmm_rob): the fast solver, redone robustly when not clean
+  IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
                                                           RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w,
                                                           best, 50, HS_TOL);
-  if (o.why == 7) {
-    ++g_stiff_redo;
-    o = ipm_solve_rows<MODE_CADMM, 1, IPM_ROBUST>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
-                                                  RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50,
-                                                  HS_TOL);
-  }
+  if (o.stiff) ++g_stiff_redo;
   *inband = o.inband ? 10 * o.why + 1 : 0;
   diag(o);
   for (int j = 0; j < n; ++j) {
