@@ -729,7 +729,8 @@ struct IPMOut {
 // terms are recomputed where consumed instead of being kept live.
 // ROB: the robust instantiation (stiff rows in augmented form, below).
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB>
-DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
+DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
+                                                          const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
                           int start) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
@@ -1942,7 +1943,10 @@ DAT_HD IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane
 //   IPM_ROBUST      robust
 //   IPM_FAST_REDO   the C-ADMM agent QP's definition: fast, redone robustly when not clean (k_cadmm_rob, the
 //                   single-QP surfaces, host builds)
-enum { IPM_FAST = 0, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
+//   IPM_FAST_R      IPM_FAST as IPM_FAST_REDO's first attempt: the same arithmetic as a template instance of
+//                   its own, so that k_cadmm's IPM_FAST instance has one call site per class and is inlined
+//                   (shared with k_cadmm_rob's redo it was called, and k_cadmm took 7 % longer)
+enum { IPM_FAST = 0, IPM_FAST_R = 1, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
 // 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
 DAT_HD int ipm_rank(const IPMOut& r) { return r.status != ST_OPTIMAL ? 2 : r.inband ? 1 : 0; }
 // a fast solve k_cadmm hands over (IPM_FAST_REDO redoes it): in-band, or INACCURATE (not the solver-exception
@@ -1956,28 +1960,37 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
                         GRP grp = GRP{}) {
   if constexpr (ROBUST == IPM_FAST_REDO) {
-    const IPMOut f = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST>(sh, er, rt, P, y0, y, w, best,
-                                                                                 max_iter, tol, rw, grp);
-    if (!ipm_unclean(f)) return f;
-    IPMOut r = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                              tol, rw, grp);
-    const int rf = ipm_rank(f), rr = ipm_rank(r);
-    if (rr > rf || (rr == rf && rr == 1 && r.merit > f.merit)) {
-      // the robust outcome is worse: the fast solve once more (deterministic: it reproduces f; keeping f's
-      // iterate instead would hold another y, w, pi, u live across the robust solve)
-      const IPMOut g = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST>(sh, er, rt, P, y0, y, w, best,
-                                                                                   max_iter, tol, rw, grp);
-      const int ri = r.iters, rf2 = r.refs, rc = r.corrs;
-      r = g;
-      r.iters += ri;
-      r.refs += rf2;
-      r.corrs += rc;
+    // trip 0 fast; trip 1 robust (the fast outcome not clean); trip 2 fast once more when the robust outcome
+    // is worse (deterministic: it reproduces the first; keeping the first iterate instead would hold another
+    // y, w, pi, u live across the robust solve).  One call site per instantiation (ipm_attempt is inlined
+    // into each: an instance called from two sites is compiled out of line, which cost k_cadmm 7 %).
+    IPMOut o, f;
+    int done = 0, done_refs = 0, done_corrs = 0;
+#pragma unroll 1
+    for (int trip = 0;; ++trip) {
+      if (trip == 1)
+        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                           tol, rw, grp);
+      else
+        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_R>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                           tol, rw, grp);
+      o.iters += done;
+      o.refs += done_refs;
+      o.corrs += done_corrs;
+      if (trip == 2) break;
+      if (trip == 0) {
+        if (!ipm_unclean(o)) break;
+        f = o;
+      } else {
+        const int rf = ipm_rank(f), rr = ipm_rank(o);
+        if (!(rr > rf || (rr == rf && rr == 1 && o.merit > f.merit))) break;
+      }
+      done = o.iters;
+      done_refs = o.refs;
+      done_corrs = o.corrs;
     }
-    r.iters += f.iters;
-    r.refs += f.refs;
-    r.corrs += f.corrs;
-    r.stiff = 1;  // redone robustly
-    return r;
+    o.stiff = 1;  // redone robustly
+    return o;
   } else {
     constexpr bool ROB = ROBUST == IPM_ROBUST;
     // First start: tuned for the C-ADMM agent QPs of the warm closed loop (P.tuned), conservative otherwise.
