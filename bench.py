@@ -120,6 +120,10 @@ def parse():
     ap.add_argument("--qp-tol", type=float, default=1e-10,
                     help="IPM stopping tolerance of the QPs (default 1e-10; 1e-8 = Clarabel's default, which "
                          "the reference runs with)")
+    ap.add_argument("--sustained-steps", type=int, default=1000,
+                    help="after the timed steps: the closed loop from the start states over this many HL steps "
+                         "(SURVEY 8(d)'s 10 s), reported per block of --sustained-block steps (stats.sustained); 0: off")
+    ap.add_argument("--sustained-block", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--selftest", action="store_true",
@@ -186,7 +190,8 @@ def cpu_baseline_qp(cfg: str, n: int, mode: str, budget_s: float, fixed_work: bo
                       f"{solves} {'centralized' if mode == 'centralized' else 'agent'} QPs in {dt:.1f} s"}
 
 
-def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: int, steps: int, batch: int):
+def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: int, steps: int, batch: int,
+                 late_steps: int = 0, late_block: int = 100):
     """The C4 closed loop on this host's cores (cpu_baseline/: the same per-scenario C-ADMM loop and
     per-lane fp64 code as the GPU, OpenMP over scenarios, -O3 x86-64-v3), work-matched to the GPU
     line: the first S of rank 0's scenarios -- the same start states, forests and controller -- run
@@ -194,7 +199,9 @@ def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: in
     acceleration + C-ADMM control + 10 simulation steps), so the CPU solves the same agent QPs from the
     same warm states as the GPU's timed region (S = all of them unless that exceeds ~budget_s; a
     1-step calibration on a small subset sizes S).  Once on all OpenMP threads of this process (the
-    reported value) and once on 1 thread (the first 64 scenarios)."""
+    reported value) and once on 1 thread (the first 64 scenarios).  late_steps > 0: the late loop as well
+    (late_loop): the first S2 scenarios run HL steps [0, late_steps - late_block) untimed and the last block
+    timed, the window of the GPU's last sustained block (S2 sized to ~1/4 of budget_s at the warm rate)."""
     import cpu_baseline as cb
     from distributed_aerial_transportation_amd import Forest, scenarios
 
@@ -234,13 +241,28 @@ def cpu_baseline(n: int, budget_s: float, start: str, forests_n: int, warmup: in
     q1, _ = c1.closed_loop(steps, threads=1)
     t1 = time.perf_counter() - t0
     c1.close()
+    late = None
+    if late_steps > late_block > 0:
+        rate_warm = S * steps / max(tN, 1e-6)  # scenario-steps per second of the timed (warm) steps
+        S2 = int(min(batch, max(threads, 0.25 * budget_s * rate_warm / late_steps)))
+        c2 = ctx(S2)
+        c2.closed_loop(late_steps - late_block, threads=threads)
+        t0 = time.perf_counter()
+        q2, i2 = c2.closed_loop(late_block, threads=threads)
+        t2 = time.perf_counter() - t0
+        c2.close()
+        late = {"value": q2 / t2, "unit": "agent-QP solves/s", "cores": threads,
+                "ms_per_scenario_step": t2 * 1e3 / (S2 * late_block) * threads,
+                "sample": f"the first {S2} scenarios, HL steps {late_steps - late_block}-{late_steps - 1} of the "
+                          f"closed loop from the start states ({q2} agent QPs, {i2 / max(q2, 1):.2f} IPM it/QP, "
+                          f"{t2:.1f} s on {threads} threads)"}
     try:
         cpu = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except (OSError, IndexError):
         cpu = "unknown"
     return {"value": qN / tN, "unit": "agent-QP solves/s", "cores": threads, "affinity_cpus": affinity,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "kind": "port", "single_core_value": q1 / t1, "ipm_iters_per_qp": iN / max(qN, 1),
+            "kind": "port", "single_core_value": q1 / t1, "ipm_iters_per_qp": iN / max(qN, 1), "late_loop": late,
             "sample": f"C++ OpenMP restatement of the C4 loop (cpu_baseline/dat_cpu.hip, same per-lane code as the "
                       f"kernels), n={n}: the first {S} of the bench's {batch} {start}-start scenarios (rank 0), "
                       f"{warmup} untimed + {steps} timed HL steps like the GPU line ({qN} agent QPs, "
@@ -381,6 +403,48 @@ def timed_steps(eng, steps: int, barrier):
     return t1 - t0, per
 
 
+def sustained_loop(eng, states, steps: int, block: int, barrier, dist, dev, n: int, batch_all: int) -> dict:
+    """SURVEY 8(d)'s sustained rate: the closed loop from the start states (warm state reset) over `steps` HL
+    steps, timed per block of `block` steps like the timed region (barrier + device synchronisation around
+    one dat_closed_loop call; max over ranks, counters summed).  The late blocks hold the stalled ADMM loops
+    next to trees that the short timed region does not reach (their agent QPs take the robust redo)."""
+    eng.reset_warm_start()
+    eng.set_state(states, np.zeros(len(states), dtype=np.int32))
+    rows = []
+    for b0 in range(0, steps, block):
+        k = min(block, steps - b0)
+        eng.reset_counters()
+        barrier()
+        eng.synchronize()
+        t0 = time.perf_counter()
+        eng.closed_loop(k)
+        eng.synchronize()
+        dt = time.perf_counter() - t0
+        barrier()
+        w = eng.work()
+        rows.append([dt, w["qp_solves"], w["ipm_iters"], w.get("inband_exits", 0),
+                     w.get("inband_beyond_clarabel_tol", 0), w.get("robust_redos", 0), k])
+    rows = np.array(rows, dtype=np.float64)
+    if dist is not None:
+        from distributed_aerial_transportation_amd.sharding import reduce_values
+
+        mx = reduce_values(rows.reshape(-1), "max", dev).reshape(rows.shape)
+        rows = reduce_values(rows.reshape(-1), "sum", dev).reshape(rows.shape)
+        rows[:, 0], rows[:, 6] = mx[:, 0], mx[:, 6]
+    blocks = []
+    b0 = 0
+    for dt, q, ip, ib, lo, rr, k in rows:
+        blocks.append({"hl_steps": f"{b0}-{b0 + int(k) - 1}", "ms_per_step": dt / k * 1e3, "qp_per_s": q / dt,
+                       "mean_admm_passes": q / (batch_all * n * k), "ipm_iters_per_qp": ip / max(q, 1),
+                       "inband_exits": int(ib), "inband_beyond_clarabel_tol": int(lo), "robust_redos": int(rr)})
+        b0 += int(k)
+    T, Q = rows[:, 0].sum(), rows[:, 1].sum()
+    return {"hl_steps": steps, "block": block, "ms_per_step": T / steps * 1e3, "qp_per_s": Q / T,
+            "slowest_block_ms_per_step": max(b["ms_per_step"] for b in blocks),
+            "inband_beyond_clarabel_tol": int(rows[:, 4].sum()), "robust_redos": int(rows[:, 5].sum()),
+            "blocks": blocks}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -459,6 +523,9 @@ def main():
         all_metrics = local_metrics
         qps_all, ipm_all, row_all, hl_ms_rank0 = float(qps), float(ipm), float(row_it), float(hl_ms)
         inband_all, scen_all, loose_all = int(tot[5]), B, int(tot[7])
+    sust = None
+    if args.sustained_steps > 0 and not args.selftest:
+        sust = sustained_loop(eng, states, args.sustained_steps, args.sustained_block, barrier, dist, dev, n, scen_all)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -535,7 +602,9 @@ def main():
                   # 1e-8 tolerance (dat_get_inband_exits)
                   "inband_exits": inband_all, "inband_beyond_clarabel_tol": loose_all,
                   # scenario-steps k_cadmm handed to k_cadmm_rob (an agent QP turned stiff), rank 0
-                  "robust_redos": int(work.get("robust_redos", 0))},
+                  "robust_redos": int(work.get("robust_redos", 0)),
+                  # the 10 s closed loop from the start states, per block of HL steps (sustained_loop)
+                  "sustained": sust},
         "roofline": {"bound": "fp64-valu", "achieved": achieved_tflops, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "kernel": kernel, "launch_ms": kernel_ms,
@@ -546,7 +615,8 @@ def main():
     }
     # (the CPU restatement solves at the default 1e-10: no work-matched baseline at another --qp-tol)
     if not args.no_cpu_baseline and world == 1 and not args.selftest and args.qp_tol == 1e-10:
-        out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start, args.forests, args.warmup, args.steps, B)
+        out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start, args.forests, args.warmup, args.steps, B,
+                                           args.sustained_steps, args.sustained_block)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

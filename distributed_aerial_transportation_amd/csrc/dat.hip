@@ -90,7 +90,7 @@ __host__ __device__ constexpr int cadmm_nr(int cls) { return NBASE + class_env_r
 // doubles rounded up to a 16-byte multiple: every LDS region starts 16-byte aligned (pair reads)
 __host__ __device__ constexpr size_t al2(size_t d) { return (d + 1) & ~(size_t)1; }
 // per-slot ints done / sid / wmx (G each), rounded to 16 bytes
-__host__ __device__ constexpr int slot_ints(int G) { return (4 * G + 3) & ~3; }
+__host__ __device__ constexpr int slot_ints(int G) { return (3 * G + 3) & ~3; }
 __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
   return sizeof(double) * (al2((size_t)G * 3 * n) + (size_t)G * RT_STRIDE * n) + sizeof(QPShared) * (size_t)G +
          sizeof(int) * (size_t)slot_ints(G);
@@ -138,8 +138,6 @@ struct CadmmLds {
   int* done;  // per slot: the scenario stopped in this pass
   int* sid;   // per slot: scenario id, -1 empty, -2 retired (queue drained)
   int* wmx;   // per slot: IPM iterations of the scenario's slowest agent QP so far this step
-  int* flag;  // per slot: k_cadmm: lanes whose solve was not clean (to k_cadmm_rob); k_cadmm_rob: redone robustly
-              // were used this step
 };
 __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int rmode) {
   CadmmLds L;
@@ -149,7 +147,6 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.done = (int*)(L.sh + G);
   L.sid = L.done + G;
   L.wmx = L.sid + G;
-  L.flag = L.wmx + G;
   L.rows = (double*)(L.done + slot_ints(G));
   L.red = L.rows;
   const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
@@ -445,12 +442,13 @@ struct WaveCounters {
 // fixed group stops (SIMD occupancy: dat_get_class_occupancy).  A scenario's arithmetic does not
 // depend on which slot or wavefront runs it.
 // Every agent QP is solved as ipm_solve IPM_FAST_REDO defines it: the fast solver, redone by the robust one
-// when it does not end cleanly.  RB = false (k_cadmm) carries only the fast solver (IPM_FAST): a scenario one
-// of whose agent QPs does not end cleanly leaves at the end of that pass's solves with a resume record (rres)
-// and goes to its class's robust list, and so does a scenario whose previous step needed the robust solver
-// (rflag: routing only).  RB = true (k_cadmm_rob, launched after k_cadmm) drains the
-// robust lists with IPM_FAST_REDO, resuming each scenario in the pass it left (re-solving there only the
-// agent QPs handed over), so a scenario's arithmetic does not depend on which kernel ran which pass.
+// when it does not end cleanly (ipm_unclean).  RB = false (k_cadmm) carries only the fast solver (IPM_FAST): a
+// scenario one of whose agent QPs does not end cleanly leaves at the end of that pass's solves with a resume
+// record (rres) and goes to its class's robust list.  RB = true (k_cadmm_rob, launched after k_cadmm) drains
+// the robust lists with IPM_FAST_REDO, resuming each scenario in the pass it left (re-solving there only the
+// agent QPs handed over) and finishing its step (and its later fused steps).  Built with -ffp-contract=on
+// (multiply-adds fused within an expression only), the inlined solver computes the same bits in either
+// kernel, so a scenario's results do not depend on which kernel ran which pass.
 template <int CLS, bool RB>
 __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr bool ENV = CLS > 0;
@@ -501,18 +499,11 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       for (;;) {
         const int q = atomicAdd(qh, 1);
         s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
-        if (RB || s2 < 0 || !a.rflag[s2]) break;
-        int* const rr = a.rres + (size_t)s2 * RRES_INTS;  // straight to k_cadmm_rob, from the step's start
-        rr[RRES_KSTEP] = 0;
-        rr[RRES_PASS] = 0;
-        rr[RRES_WMX] = 0;
-        rr[RRES_LANES] = -1;
-        a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = s2;
+        break;
       }
       L.sid[ls] = s2;
       L.done[ls] = 0;
       L.wmx[ls] = RB && s2 >= 0 ? a.rres[(size_t)s2 * RRES_INTS + RRES_WMX] : 0;
-      L.flag[ls] = 0;
     }
     __syncthreads();
     const int slot_sc = lane < NT ? L.sid[ls] : -2;
@@ -571,7 +562,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     DAT_PHASE(14);
     bool active = slot_sc >= 0;
     int it_lane = 0;
-    bool hand = false;  // k_cadmm: this lane's solve was not clean; k_cadmm_rob: it was redone robustly
+    bool hand = false;  // k_cadmm: this lane's solve was not clean (ipm_unclean)
     if (active && ((rmask >> i) & 1)) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho, RT_STRIDE);
       DAT_PHASE(15);
@@ -597,7 +588,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowRegs, 0, NoGrp, RM>(
             shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol);
       }
-      hand = RB ? o.stiff != 0 : ipm_unclean(o);
+      hand = !RB && ipm_unclean(o);
       DAT_PHASE(9);
       wc.ipm += o.iters;
       wc.inband += o.inband;
@@ -628,11 +619,9 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     ++wc.pass;
     if (active) atomicMax(&L.wmx[ls], it_lane);
     rmask = -1;
-    // the slot's lanes whose solve k_cadmm hands over (a ballot: the block is one wavefront; an LDS flag set
-    // in the solve block cost k_cadmm ~65 % more scratch); k_cadmm_rob: the step redid a solve (routing)
+    // the slot's lanes whose solve k_cadmm hands over (a ballot: the block is one wavefront)
     const unsigned long long hb = __ballot(hand);
     const int hmask = lane < NT ? (int)((hb >> (ls * n)) & ((1ull << n) - 1ull)) : 0;
-    if (RB && hand) L.flag[ls] = 1;
     __syncthreads();
     if (!RB && active && hmask) {
       // an agent QP of the pass was not clean: k_cadmm_rob resumes the scenario here (the mean of the pass's
@@ -726,10 +715,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
       } else {
         // the scenario stopped: write its outputs and free the slot
-        if (RB && i == 0) {
-          a.rflag[sc] = L.flag[ls] != 0;  // the next step goes straight to k_cadmm_rob only if this one needed it
-          atomicAdd(a.counters + CNT_ROB, 1ull);
-        }
+        if (RB && i == 0) atomicAdd(a.counters + CNT_ROB, 1ull);
         for (int c = 0; c < 3; ++c) {
           a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
           a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
@@ -751,7 +737,6 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
             build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
                          prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
             L.wmx[ls] = 0;
-            L.flag[ls] = 0;  // k_cadmm_rob: whether this step redoes a solve robustly (the routing of the next)
           }
         } else if (i == 0) {
           L.sid[ls] = -1;
@@ -1579,7 +1564,6 @@ __global__ void k_warm(KArgs a) {
         a.clam[((size_t)sc * n + i) * N3 + c] = 0.0;
       }
     for (int c = 0; c < N3; ++c) a.cfbar[(size_t)sc * N3 + c] = feq[c];
-    if (a.rflag) a.rflag[sc] = 0;
   }
   if (a.dlamF) {
     double s3[3] = {0, 0, 0};
@@ -1754,7 +1738,7 @@ struct dat_handle {
   double* mountain = nullptr;
   int nforest = 0;
   double *cf = nullptr, *cfbar = nullptr, *clam = nullptr;
-  int *rlist = nullptr, *rflag = nullptr, *rres = nullptr;  // C-ADMM: robust lists, routing flags, resume records
+  int *rlist = nullptr, *rres = nullptr;  // C-ADMM: robust lists, resume records
   double *dlamF = nullptr, *dlamM = nullptr, *dprev = nullptr, *dHinv = nullptr;
   double* pf = nullptr;
   double* best = nullptr;
@@ -1870,7 +1854,6 @@ KArgs kargs(dat_handle* h) {
   a.scount = h->scount;
   a.qhead = h->scount ? h->scount + 2 * NCLS : nullptr;
   a.rlist = h->rlist;
-  a.rflag = h->rflag;
   a.rres = h->rres;
   a.ll_kind = h->ll_kind;
   return a;
@@ -1978,7 +1961,6 @@ KArgs sub_kargs(dat_handle* h, int off, int Bs, int s) {
   a.ipmx += o;
   a.slist += o;
   a.rlist += o;
-  a.rflag += o;
   a.rres += o * RRES_INTS;
   a.scount = h->scount + SCOUNT_INTS * s;
   a.qhead = a.scount + 2 * NCLS;
@@ -2103,7 +2085,6 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->clam, B * n * N3);
     rc |= dalloc(h, &h->rres, B * RRES_INTS);
     rc |= dalloc(h, &h->rlist, B);
-    rc |= dalloc(h, &h->rflag, B);
   } else if (c.mode == DAT_MODE_DD) {
     rc |= dalloc(h, &h->need, B);
     rc |= dalloc(h, &h->ipmx, B);

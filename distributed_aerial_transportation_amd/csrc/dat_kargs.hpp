@@ -87,7 +87,6 @@ struct KArgs {
   int* scount;                   // C-ADMM: [0, NCLS) class sizes, [NCLS, 2 NCLS) class start offsets
   int* qhead;                    // C-ADMM: [NCLS] queue heads of the classes (reset by k_bucket)
   int* rlist;                    // C-ADMM: scenarios whose step k_cadmm_rob redoes, by class (class starts as slist)
-  int* rflag;                    // C-ADMM: per scenario, its previous step needed the robust solver (route it there)
   int* rres;                     // C-ADMM: per listed scenario, where k_cadmm_rob resumes it (RRES_* fields)
   double* erows;                 // C-ADMM: env rows of the step per agent (k_env_class -> k_cadmm), SoA:
                                  //   [(4 j + c) B n + sc n + i], c < 3: lhs, c = 3: rhs

@@ -1949,10 +1949,11 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
 enum { IPM_FAST = 0, IPM_FAST_R = 1, IPM_ROBUST = 2, IPM_FAST_REDO = 3 };
 // 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
 DAT_HD int ipm_rank(const IPMOut& r) { return r.status != ST_OPTIMAL ? 2 : r.inband ? 1 : 0; }
-// a fast solve k_cadmm hands over (IPM_FAST_REDO redoes it): in-band, or INACCURATE (not the solver-exception
-// branch, ST_FAILED: non-finite data)
+// a fast solve k_cadmm hands over (IPM_FAST_REDO redoes it): INACCURATE (not the solver-exception branch,
+// ST_FAILED: non-finite data), or accepted through an in-band iterate outside Clarabel's own tolerance (an
+// in-band accept within it is one Clarabel would return as well)
 DAT_HD bool ipm_unclean(const IPMOut& r) {
-  return r.status == ST_INACCURATE || (r.status == ST_OPTIMAL && r.inband);
+  return r.status == ST_INACCURATE || (r.status == ST_OPTIMAL && r.inband && r.merit > IPM_CLARABEL_TOL);
 }
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0,
           class GRP = NoGrp, int ROBUST = IPM_FAST>
