@@ -180,10 +180,11 @@ def test_sm_closed_loop_matches_reference():
 def test_c4_stall_stretch_matches_oracle():
     """The C4 stall stretches of ref_c4_hard.npz (tests/golden/make_c4_hard.py, n = 6 in seeded forests,
     101-pass ADMM stalls from the second step on) with every agent QP answered by the host build of the
-    device solver as the GPU's C-ADMM step runs it (the fast solver, redone robustly when a row turns
-    stiff): ADMM iteration counts exact and f_des within max(1e-5, 5 x the oracle's own sensitivity) at
-    every step.  The first 12 steps of both stretches (the round-4 solver left the oracle by 2e-4 at steps
-    16-17 of the second; the GPU test runs all 20)."""
+    device solver as the GPU's C-ADMM step runs it (IPM_FAST_REDO: the fast solver, redone robustly when
+    not clean): ADMM iteration counts exact and f_des within max(1e-5, 5 x the oracle's own sensitivity)
+    at every step (or the reference's own spread at Clarabel's 1e-8, f_des_1e8).  The first 12 steps of
+    both stretches (the round-4 solver left the oracle by 2e-4 at steps 16-17 of the second; the GPU test
+    runs all 20)."""
     from distributed_aerial_transportation_amd import scenarios
     from distributed_aerial_transportation_amd.system import RQPState, pack_state
     from oracle import controllers as oc
@@ -225,7 +226,8 @@ def test_c4_stall_stretch_matches_oracle():
             ref = d["f_des"][j, k]
             scale = max(1.0, np.max(np.abs(ref)))
             sens = np.max(np.abs(d["f_des_1e10"][j, k] - ref)) / scale
-            assert np.max(np.abs(f - ref)) / scale < max(1e-5, 5.0 * sens), (j, k)
+            sens8 = np.max(np.abs(d["f_des_1e8"][j, k] - ref)) / scale  # the reference at Clarabel's 1e-8
+            assert np.max(np.abs(f - ref)) / scale < max(1e-5, 5.0 * sens, sens8), (j, k)
             for _ in range(10):
                 fl, M = om.low_level_control(p, st, f)
                 st.integrate(*om.forward_dynamics(p, st, fl, M), 1e-3)

@@ -11,7 +11,7 @@ B=${B:-65536}
 # B=default: the bench's own default workload (65,536 scenarios, strong split), whose workload string
 # profiles/traffic.json is keyed on
 BATCH_ARG="--batch $B"; [ "$B" = "default" ] && BATCH_ARG=""
-ARGS="$R/bench.py --steps ${STEPS:-5} --warmup ${WARMUP:-2} $BATCH_ARG --no-cpu-baseline ${EXTRA:-}"
+ARGS="$R/bench.py --steps ${STEPS:-5} --warmup ${WARMUP:-2} $BATCH_ARG --no-cpu-baseline --sustained-steps 0 ${EXTRA:-}"
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 $ARGS > $OUT/kt.log 2>&1 || exit 11
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --kernel-trace -d $OUT/pmc1 -o run --output-format csv -- python3 $ARGS > $OUT/pmc1.log 2>&1 || exit 12
