@@ -1777,8 +1777,6 @@ struct dat_handle {
 int cadmm_slots(const dat_handle* h, int B, int n) {
   const int gmax = 64 / n;
   int pb = h->persistent_blocks / 4 > 0 ? h->persistent_blocks / 4 : 1;
-  if (const char* e = getenv("DAT_SLOT_BLOCKS"))  // development knob (small-batch experiments)
-    if (atoi(e) > 0) pb = atoi(e);
   const int g = (B + pb - 1) / pb;
   return g < 1 ? 1 : (g > gmax ? gmax : g);
 }
@@ -2059,8 +2057,6 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device) == hipSuccess && ncu > 0)
     h->persistent_blocks = 4 * ncu;  // k_cadmm: one wavefront per SIMD (register-bound), 4 SIMDs per CU
-  if (const char* e = getenv("DAT_WAVES_PER_CU"))  // development knob (occupancy experiments)
-    if (atoi(e) > 0 && ncu > 0) h->persistent_blocks = atoi(e) * ncu;
   const size_t B = c.batch, n = c.n, N3 = 3 * n;
   int rc = 0;
   rc |= dalloc(h, &h->state, B * h->S);

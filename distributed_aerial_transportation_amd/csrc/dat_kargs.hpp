@@ -9,10 +9,7 @@ namespace dat {
 constexpr int NMAX = 16;        // largest team the kernels are compiled for
 constexpr int NMAX_DD = 16;     // DD: k_dd_setup<0> keeps [H | I] (2 (6n)^2 doubles) in LDS: 144 KB at n = 16
 constexpr int IPM_MAX_ITER = 50;
-#ifndef DAT_IPM_TOL
-#define DAT_IPM_TOL 1e-10
-#endif
-constexpr double IPM_TOL = DAT_IPM_TOL;  // default IPM stopping tolerance (dat_set_qp_tolerance)
+constexpr double IPM_TOL = 1e-10;  // default IPM stopping tolerance (dat_set_qp_tolerance)
 // C-ADMM env classes (cadmm_block<C>): 0 no env row, then the largest per-agent env-row count of the
 // scenario's QPs <= 2, <= 5, <= DAT_NENV.  Row slots of class C: NBASE + CLASS_ENV[C].
 constexpr int NCLS = 4;

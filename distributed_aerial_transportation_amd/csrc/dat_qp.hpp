@@ -31,46 +31,25 @@ namespace dat {
 
 constexpr int NWROW = 2;          // slots [0, NWROW) act on dwl
 constexpr int NBASE = 3;          // base slots shared by all agents of a scenario
-#ifndef DAT_IPM_NREF
-#define DAT_IPM_NREF 6
-#endif
 // iterative-refinement passes per corrector solve (at most; a pass stops the loop once the linearised
 // system is solved to rounding, so well-scaled QPs run one).  Badly scaled agent QPs -- consensus
 // multipliers ~1e3-1e4 in a stalled ADMM loop, active rows with barrier weights z/s ~1e15 -- need up to
 // six to keep the dual residual below the stopping tolerance (tools/hard_qp_probe.py: 2 passes left
 // 281 of 798 such solves at in-band exits, 6 passes 69, all within 1.5e-6 of the oracle)
-constexpr int NREF = DAT_IPM_NREF;
-// Initial point: cone / row slacks shifted to at least DAT_IPM_S0 inside, duals DAT_IPM_Z0 e.  The
-// agent QPs' multipliers are O(1e-2) at the solution; starting the duals and the slack margins there
-// instead of at 1 takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU
-// sweep over {0.01, 0.03, 0.1, 0.3, 1, 3, 10}^2, tools/ipm_init_sweep.py; same solutions to the
-// solver tolerance).
-#ifndef DAT_IPM_S0
-#define DAT_IPM_S0 0.03
-#endif
-#ifndef DAT_IPM_Z0
-#define DAT_IPM_Z0 0.03
-#endif
-// divergence stop (from the 5th iteration): merit above DAT_IPM_DIVERGE x the best seen.  A start
-// close to the boundary can raise the residuals by 1e3 in its first steps on a well-posed DD QP.
-// DD agent QPs: the conservative start.  Development knobs; round-3 A/B on C3 (IPM it/QP, ms per step
-// against 9.46, 20.3 / 20.7): S0 = Z0 = 0.3 -> 9.00, 21.4; 0.1 -> 8.89, 22.0; ETA 0.995 -> 9.29, 20.9;
-// 0.1 and 0.995 -> 8.71, 21.8 -- fewer iterations on average, a wider spread across a wavefront.
-#ifndef DAT_DD_S0
-#define DAT_DD_S0 1.0
-#endif
-#ifndef DAT_DD_Z0
-#define DAT_DD_Z0 1.0
-#endif
-#ifndef DAT_DD_ETA
-#define DAT_DD_ETA 0.99
-#endif
-#ifndef DAT_IPM_ETA
-#define DAT_IPM_ETA 0.999  // fraction of the step to the cone boundary (7.00 -> 5.23 -> 4.28 it/QP)
-#endif
-#ifndef DAT_IPM_DIVERGE
-#define DAT_IPM_DIVERGE 1e6
-#endif
+constexpr int NREF = 6;
+// Initial point: cone / row slacks shifted to at least IPM_S0 inside, duals IPM_Z0 e.  The agent QPs'
+// multipliers are O(1e-2) at the solution; starting the duals and the slack margins there instead of at 1
+// takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU sweep over
+// {0.01, 0.03, 0.1, 0.3, 1, 3, 10}^2, tools/ipm_init_sweep.py; same solutions to the solver tolerance).
+constexpr double IPM_S0 = 0.03, IPM_Z0 = 0.03;
+constexpr double IPM_ETA = 0.999;  // fraction of the step to the cone boundary (7.00 -> 5.23 -> 4.28 it/QP)
+// DD agent QPs: the conservative start.  Round-3 A/B on C3 (IPM it/QP, ms per step against 9.46,
+// 20.3 / 20.7): S0 = Z0 = 0.3 -> 9.00, 21.4; 0.1 -> 8.89, 22.0; ETA 0.995 -> 9.29, 20.9; 0.1 and 0.995 ->
+// 8.71, 21.8 -- fewer iterations on average, a wider spread across a wavefront.
+constexpr double DD_S0 = 1.0, DD_Z0 = 1.0, DD_ETA = 0.99;
+// divergence stop (from the 5th iteration): merit above IPM_DIVERGE x the best seen.  A start close to
+// the boundary can raise the residuals by 1e3 in its first steps on a well-posed DD QP.
+constexpr double IPM_DIVERGE = 1e6;
 
 // Every array starts on a 16-byte boundary and the kernels place the record 16-byte aligned in LDS,
 // so the solver reads entry pairs (ldn: one ds_read_b128 per pair).
@@ -940,9 +919,9 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
   // second start of a DD / centralized solve that ended outside Clarabel's tolerance, see ipm_solve)
   const bool TUNED = MODE == MODE_CADMM && start == 1;
   const double SCL = start == 2 ? 10.0 : 1.0;
-  const double S0 = SCL * (TUNED ? DAT_IPM_S0 : MODE == MODE_DD ? DAT_DD_S0 : 1.0);
-  const double Z0 = SCL * (TUNED ? DAT_IPM_Z0 : MODE == MODE_DD ? DAT_DD_Z0 : 1.0);
-  const double ETA = TUNED ? DAT_IPM_ETA : MODE == MODE_DD ? DAT_DD_ETA : 0.99;
+  const double S0 = SCL * (TUNED ? IPM_S0 : MODE == MODE_DD ? DD_S0 : 1.0);
+  const double Z0 = SCL * (TUNED ? IPM_Z0 : MODE == MODE_DD ? DD_Z0 : 1.0);
+  const double ETA = TUNED ? IPM_ETA : MODE == MODE_DD ? DD_ETA : 0.99;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
 #pragma unroll
@@ -1159,7 +1138,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
         }
       }
       BM() = fmin(BM(), merit);
-      if ((it >= 4 && merit > DAT_IPM_DIVERGE * BM()) || it >= max_iter) {
+      if ((it >= 4 && merit > IPM_DIVERGE * BM()) || it >= max_iter) {
         out.why = 2;
         break;
       }

@@ -1,17 +1,28 @@
-# IPM initial-point sweep on the CPU (dev tool): builds the C++ C4 closed loop (cpu_baseline/) with
-# -DDAT_IPM_Z0=.. -DDAT_IPM_S0=.. and reports IPM iterations per agent QP over warm HL steps.
-#   python tools/ipm_init_sweep.py <tag> [-DDAT_IPM_Z0=0.03 -DDAT_IPM_S0=0.03]
+# IPM initial-point sweep on the CPU (dev tool): builds the C++ C4 closed loop (cpu_baseline/) from a copy of
+# its sources with the tuned start's constants (IPM_S0, IPM_Z0 in dat_qp.hpp) replaced, and reports IPM
+# iterations per agent QP over warm HL steps.
+#   python tools/ipm_init_sweep.py <tag> [S0 Z0]
 import sys, os, subprocess, ctypes, time
 sys.path.insert(0, '/root/repo')
 import numpy as np
 import cpu_baseline as cb
 from distributed_aerial_transportation_amd import Forest, scenarios
 import bench
-tag, flags = sys.argv[1], sys.argv[2:]
+import re
+import shutil
+tag = sys.argv[1]
+s0, z0 = (sys.argv[2], sys.argv[3]) if len(sys.argv) > 3 else ("0.03", "0.03")
 lib = f'/tmp/cb_{tag}.so'
 if not os.path.exists(lib):
+    src = f'/tmp/cb_{tag}_src'
+    shutil.rmtree(src, ignore_errors=True)
+    shutil.copytree('/root/repo', src, ignore=shutil.ignore_patterns('.git', 'gpurun_out', 'diag', '*.so', '*.npz'))
+    qp = os.path.join(src, 'distributed_aerial_transportation_amd', 'csrc', 'dat_qp.hpp')
+    t = open(qp).read()
+    t = re.sub(r"constexpr double IPM_S0 = [^,]*, IPM_Z0 = [^;]*;", f"constexpr double IPM_S0 = {s0}, IPM_Z0 = {z0};", t)
+    open(qp, 'w').write(t)
     subprocess.check_call(["hipcc", "-O3", "-march=x86-64-v3", "-fopenmp", "-std=c++17", "-fPIC", "-shared",
-                           "--offload-arch=gfx950", *flags, cb.SRC, "-o", lib])
+                           "--offload-arch=gfx950", os.path.join(src, os.path.relpath(cb.SRC, '/root/repo')), "-o", lib])
 cb.LIB = lib
 n, S, F = 6, 768, 64
 scen_forest, seed = bench.shard(0, S, F)
