@@ -1869,16 +1869,19 @@ size_t dd_setup_lds(int n) {
 }
 
 // the C-ADMM drain of one control step: k_cadmm (env classes 3, 2, 1, 0) with a forest, k_cadmm0 without
-// k_cadmm_rob: blocks of the robust redo (the listed scenarios are few: stalls next to trees)
+// k_cadmm_rob: blocks of the robust redo, one scenario slot each (G = 1).  The listed scenarios are few --
+// stalled ADMM loops next to trees, 101 sequential passes -- and run after k_cadmm: a slot of its own per
+// scenario keeps one scenario's pass from waiting for the slowest agent QP of the others'.
 constexpr int ROB_BLOCKS = 256;
 void launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st) {
-  const int rblocks = std::min(blocks, ROB_BLOCKS);
+  KArgs r = a;
+  r.G = 1;
   if (h->nforest > 0) {
     hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
-    hipLaunchKernelGGL(k_cadmm_rob, dim3(rblocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
+    hipLaunchKernelGGL(k_cadmm_rob, dim3(ROB_BLOCKS), dim3(64), cadmm_lds_bytes(r.n, r.G, NCLS - 1), st, r);
   } else {
     hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
-    hipLaunchKernelGGL(k_cadmm0_rob, dim3(rblocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
+    hipLaunchKernelGGL(k_cadmm0_rob, dim3(ROB_BLOCKS), dim3(64), cadmm_lds_bytes(r.n, r.G, 0), st, r);
   }
 }
 

@@ -1959,7 +1959,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       o.corrs += done_corrs;
       if (trip == 2) break;
       if (trip == 0) {
-        if (!ipm_unclean(o)) break;
+        if (!ipm_unclean(o)) return o;
         f = o;
       } else {
         const int rf = ipm_rank(f), rr = ipm_rank(o);
