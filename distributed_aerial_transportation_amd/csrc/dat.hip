@@ -590,17 +590,20 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }
       hand = !RB && ipm_unclean(o);
       DAT_PHASE(9);
-      wc.ipm += o.iters;
-      wc.inband += o.inband;
+      // a solve k_cadmm hands over is counted once, by k_cadmm_rob (its IPM_FAST_REDO runs the fast attempt
+      // again): its discarded outcome here is neither an agent-QP solve nor an in-band accept
+      const int keep = hand ? 0 : 1;
+      wc.ipm += keep * o.iters;
+      wc.inband += keep * o.inband;
 #ifdef DAT_ITER_HIST
       atomicAdd(&g_iter_hist[o.iters < 63 ? o.iters : 63], 1ull);
 #endif
-      wc.loose += inband_loose(o);
-      wc.refs += o.refs;
-      wc.corrs += o.corrs;
+      wc.loose += keep * inband_loose(o);
+      wc.refs += keep * o.refs;
+      wc.corrs += keep * o.corrs;
       it_lane = o.iters;
-      wc.rowit += (long long)o.iters * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
-      ++wc.qp;
+      wc.rowit += (long long)(keep * o.iters) * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
+      wc.qp += keep;
       qstat = o.status;
       if (o.status == ST_OPTIMAL) {
         for (int j = 0; j < n; ++j) {
