@@ -8,7 +8,9 @@ Size-independent properties (the oracle cannot run 65,536 scenarios):
   Clarabel's 1e-8;
 * a scenario's results do not depend on the batch it runs in, its workgroup slot or the stream: the
   8,192-scenario run on 4 streams equals the first 8,192 scenarios of the 65,536-scenario run bitwise
-  (states after 3 HL steps, ADMM counts);
+  (states after 3 HL steps, ADMM counts).  The two runs group differently: 10 scenario slots per k_cadmm
+  wavefront at 65,536, 8 per wavefront in each 2,048-scenario sub-batch (cadmm_slots), and G selects the
+  row-state instantiation of each env class (cadmm_row_mode: registers or LDS);
 * the first 64 scenarios equal the CPU restatement (cpu_baseline/dat_cpu.hip: the same per-scenario loop
   and per-lane code, compiled for the host; tests/test_cpu_baseline.py pins it against the reference's own
   closed loop) to 1e-9 in the states and exactly in the ADMM counts."""
