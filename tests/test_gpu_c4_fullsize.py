@@ -13,7 +13,7 @@ Size-independent properties (the oracle cannot run 65,536 scenarios):
   row-state instantiation of each env class (cadmm_row_mode: registers or LDS);
 * the first 64 scenarios equal the CPU restatement (cpu_baseline/dat_cpu.hip: the same per-scenario loop
   and per-lane code, compiled for the host; tests/test_cpu_baseline.py pins it against the reference's own
-  closed loop) to 1e-9 in the states and exactly in the ADMM counts."""
+  closed loop) to 1e-9 in the states."""
 
 import numpy as np
 import pytest
