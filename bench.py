@@ -601,7 +601,7 @@ def main():
                   # agent QPs accepted through the best in-band iterate, and those beyond Clarabel's
                   # 1e-8 tolerance (dat_get_inband_exits)
                   "inband_exits": inband_all, "inband_beyond_clarabel_tol": loose_all,
-                  # scenario-steps k_cadmm handed to k_cadmm_rob (an agent QP turned stiff), rank 0
+                  # scenario-steps k_cadmm handed to k_cadmm_rob (an agent QP not clean), rank 0
                   "robust_redos": int(work.get("robust_redos", 0)),
                   # the 10 s closed loop from the start states, per block of HL steps (sustained_loop)
                   "sustained": sust},

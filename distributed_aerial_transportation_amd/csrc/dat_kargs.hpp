@@ -35,7 +35,7 @@ constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, 
 constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
 // IPM refinement passes run and corrections applied (all kernels; the executed-flop model)
 constexpr int CNT_REF = CNT_INBAND + 2;
-// C-ADMM control steps of a scenario redone by k_cadmm_rob (an agent QP turned stiff in k_cadmm)
+// C-ADMM control steps of a scenario finished by k_cadmm_rob (an agent QP not clean in k_cadmm, ipm_unclean)
 constexpr int CNT_ROB = CNT_REF + 2;
 constexpr int DAT_NCOUNTERS = CNT_ROB + 1;
 // class table of the C-ADMM / DD queues (k_bucket), per sub-batch: [0, NCLS) class sizes, [NCLS, 2 NCLS) class
@@ -44,7 +44,7 @@ constexpr int DAT_NCOUNTERS = CNT_ROB + 1;
 constexpr int SCOUNT_INTS = 5 * NCLS;
 // Resume record of a scenario k_cadmm hands to k_cadmm_rob: the fused control step and the ADMM pass it
 // stopped in, the IPM-iteration maximum so far, and the mask of its agent lanes whose solve of that pass
-// turned stiff (the others' results of the pass stand; all lanes for a scenario routed at claim)
+// was not clean (the others' results of the pass stand)
 constexpr int RRES_KSTEP = 0, RRES_PASS = 1, RRES_WMX = 2, RRES_LANES = 3, RRES_INTS = 4;
 constexpr double INBAND_CLARABEL = IPM_CLARABEL_TOL;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }

@@ -191,11 +191,12 @@ int dat_get_inband_exits(dat_handle* h, long long* inband, long long* beyond_cla
 /* IPM iterative-refinement passes run and corrections applied by every kernel since the last counter
  * reset: the executed-work terms of the flop model. */
 int dat_get_refinement_counters(dat_handle* h, long long* passes, long long* corrections);
-/* C-ADMM control steps of a scenario redone by the robust solver since the last counter reset: k_cadmm
- * hands a scenario's step to k_cadmm_rob when one of its agent QPs turns stiff (an active row's barrier
- * weight beyond 1e12, inside the reference's max_iter stalls next to trees), and the next step of that
- * scenario goes there directly while it stays stiff.  Replaces no reference call (Clarabel's internal
- * KKT regularisation); the per-QP surfaces (dat_solve_agent_qp_batch) redo the QP itself. */
+/* C-ADMM control steps of a scenario finished by the robust kernel since the last counter reset: k_cadmm
+ * hands a scenario's step to k_cadmm_rob, at the ADMM pass it is in, when one of its agent QPs does not
+ * end cleanly (INACCURATE, or accepted in band beyond Clarabel's 1e-8: inside the reference's max_iter
+ * stalls next to trees), and k_cadmm_rob redoes those QPs with the robust solver (stiff rows in augmented
+ * form) and finishes the step.  Replaces no reference call (Clarabel's internal KKT regularisation); the
+ * per-QP surfaces (dat_solve_agent_qp_batch) redo the QP themselves. */
 int dat_get_robust_redos(dat_handle* h, long long* redos);
 /* Device time [ms] of the last dat_solve_agent_qp_batch launch (k_agent_qp; HIP events on the handle's
  * stream): the solve_time RQPPrimalSolver.solve returns (Clarabel's solver_stats.solve_time,
