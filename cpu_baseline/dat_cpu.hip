@@ -67,6 +67,8 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
     double lhs[DAT_NENV][3], rhs[DAT_NENV];
     env_rows(prm, n, st, trees, nt, i, prm[DAT_P_AENVD], &emask, lhs, rhs);
     set_env_rows(P[i], E[i], S, emask, lhs, rhs);
+    // rows certified infeasible are held (the GPU's tail certifies them once per scenario-step)
+    if (dvl_rows_infeasible(PlainRef<QPShared>{&S}, EnvPlain{&E[i]}, P[i].emask)) P[i].infeasible = 1;
   }
   double* cf = c.cf.data() + (size_t)sc * n * N3;
   double* fb = c.cfbar.data() + (size_t)sc * N3;
@@ -77,13 +79,25 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
   double rho = rho0;
   int it = 0;
   const int prev_it = c.iters[sc];  // the previous step's ADMM iterations
+  // the GPU's tail rule (dat_kargs.hpp, with a forest): the warm start and stall exit of pass it >= 1 when the
+  // previous step took more than TAIL_PREV passes or it >= TAIL_PASS; the passes the tail kernel runs keep the
+  // agent QPs' warm-start records (from the step's start when routed, from the first unclean pass or TAIL_PASS)
+  const int tprev = c.nforest > 0 ? TAIL_PREV : 1 << 30, tpass = c.nforest > 0 ? TAIL_PASS : 1 << 30;
+  double wrec[NMAXC][WREC_SIZE];
+  for (int i = 0; i < n; ++i) wrec[i][0] = 0.0;
+  bool in_tail = prev_it > tprev;
   for (;;) {
+    in_tail = in_tail || it >= tpass;
+    const bool wson = it >= 1 && (prev_it > tprev || it >= tpass);
+    bool unclean = false;
     for (int i = 0; i < n; ++i) {
       lane_cadmm_dynamic(P[i], prm, n, i, Rt_all, lam + i * N3, fb, rho);
       P[i].tuned = it == 0 || prev_it <= 3;  // as k_cadmm (tuned IPM start: first pass / warm regime)
       double y[1][3], w[6], best[best_size(1)];
-      IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(rows_needed(P[i].emask), PlainRef<QPShared>{&S}, EnvPlain{&E[i]},
-                                               RtPtr{Rt_all + 9 * i}, P[i], feq + 3 * i, y, w, best, 50, 1e-10);
+      IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO, true>(
+          rows_needed(P[i].emask), PlainRef<QPShared>{&S}, EnvPlain{&E[i]}, RtPtr{Rt_all + 9 * i}, P[i], feq + 3 * i, y,
+          w, best, 50, 1e-10, in_tail ? wrec[i] : nullptr, wson);
+      unclean = unclean || o.stiff;
       ++*qp;
       *ipm += o.iters;
 #if defined(DAT_IPM_STATS)
@@ -102,6 +116,7 @@ void cadmm_step(Ctx& c, int sc, long long* qp, long long* ipm) {
         for (int k = 0; k < N3; ++k) fi[k] = feq[k];
       }
     }
+    in_tail = in_tail || (unclean && c.nforest > 0);
     ++it;
     rho = std::min(rho * tau, rho_max);
     for (int k = 0; k < N3; ++k) {

@@ -167,6 +167,8 @@ EXPORTS = {
     "dat_get_inband_exits": (ctypes.c_int, [H, LL, LL]),
     "dat_get_refinement_counters": (ctypes.c_int, [H, LL, LL]),
     "dat_get_robust_redos": (ctypes.c_int, [H, LL]),
+    "dat_get_tail_counters": (ctypes.c_int, [H, LL]),
+    "dat_get_collision_stats": (ctypes.c_int, [H, LL, D]),
     "dat_get_agent_qp_ms": (ctypes.c_int, [H, D]),
     "dat_rp_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_low_level_control": (ctypes.c_int, [H, D, D, D]),

@@ -294,9 +294,18 @@ class BatchedController:
         rr = ctypes.c_longlong()
         if hasattr(self._lib, "dat_get_robust_redos"):  # absent only from an older A/B build (DAT_LIB_PATH)
             L.check(self._lib.dat_get_robust_redos(self._h, ctypes.byref(rr)))
-        return {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
-                "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value,
-                "refine_passes": rp.value, "refine_corrections": rc.value, "robust_redos": rr.value}
+        out = {"qp_solves": q.value, "ipm_iters": it.value, "ipm_row_iters": rw.value, "hl_steps": hs.value,
+               "hl_kernel_ms": ms.value, "inband_exits": ib.value, "inband_beyond_clarabel_tol": lo.value,
+               "refine_passes": rp.value, "refine_corrections": rc.value, "robust_redos": rr.value}
+        if hasattr(self._lib, "dat_get_tail_counters"):  # absent only from an older A/B build (DAT_LIB_PATH)
+            tc = (ctypes.c_longlong * 6)()
+            L.check(self._lib.dat_get_tail_counters(self._h, tc))
+            out.update(tail_passes=tc[0], tail_critical_ipm_iters=tc[1], tail_routed=tc[2], certified_infeasible=tc[3],
+                       stall_exits=tc[4], warm_starts=tc[5])
+            col, md = ctypes.c_longlong(), ctypes.c_double()
+            L.check(self._lib.dat_get_collision_stats(self._h, ctypes.byref(col), ctypes.byref(md)))
+            out.update(collisions=col.value, min_env_dist=md.value)
+        return out
 
     def agent_qp_ms(self) -> float:
         """Device time of the last solve_agent_qps launch (dat_get_agent_qp_ms)."""

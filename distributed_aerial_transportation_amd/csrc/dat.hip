@@ -15,6 +15,7 @@
 //   k_desired  forest desired-acceleration law (example/rqp_example.py:33-59).
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -103,9 +104,14 @@ __host__ __device__ inline size_t cadmm_fixed_bytes(int n, int G) {
 // C-ADMM consensus mean and residual read agent-major, the three components of a block together
 // (bitwise equal to the component-major loops; C4 A/B: k_cadmm 3.68 / 3.63 -> 3.57 / 3.54 ms)
 __host__ __device__ constexpr unsigned cadmm_auxm(int cls) { return cls < NCLS - 1 ? 15u : 0u; }
-// row-state placement of a class: 0 registers, 1 LDS rows, 2 LDS rows + aux slots
+// row-state placement of a class: 0 registers, 1 LDS rows, 2 LDS rows + the class's aux slots, 3 LDS rows + all
+// aux slots (k_cadmm_tail: one scenario per wavefront, latency-bound, every class in LDS)
+constexpr unsigned TAIL_AUXM = 15u;
+__host__ __device__ constexpr int cadmm_aux_doubles(int cls, int rmode) {
+  return rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : rmode == 3 ? ipm_aux_doubles(1, TAIL_AUXM) : 0;
+}
 __host__ __device__ inline size_t cadmm_area_doubles(int cls, int rmode) {
-  const size_t rows = rmode ? (size_t)row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
+  const size_t rows = rmode ? (size_t)row_lds_doubles(cadmm_nr(cls), cadmm_aux_doubles(cls, rmode)) : 0;
   return (rows > 64 * RDS ? rows : 64 * RDS) + (size_t)env_lds_doubles(class_env_rows(cls));
 }
 // row state of class cls in LDS: with the class's aux slots when that carve fits the budget, else rows
@@ -131,6 +137,15 @@ __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NC
   }
   return m;
 }
+// dynamic LDS of a k_cadmm_tail workgroup (one scenario slot, rmode 3)
+__host__ __device__ inline size_t cadmm_tail_lds_bytes(int n, int max_cls = NCLS - 1) {
+  size_t m = 0;
+  for (int c = 0; c <= max_cls; ++c) {
+    const size_t b = cadmm_fixed_bytes(n, 1) + sizeof(double) * cadmm_area_doubles(c, 3);
+    m = b > m ? b : m;
+  }
+  return m;
+}
 struct CadmmLds {
   double *fbar, *Rt, *red, *rows;
   QPShared* sh;
@@ -149,7 +164,7 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   L.wmx = L.sid + G;
   L.rows = (double*)(L.done + slot_ints(G));
   L.red = L.rows;
-  const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), rmode == 2 ? ipm_aux_doubles(1, cadmm_auxm(cls)) : 0) : 0;
+  const int ra = rmode ? row_lds_doubles(cadmm_nr(cls), cadmm_aux_doubles(cls, rmode)) : 0;
   L.env = L.rows + (ra > 64 * RDS ? ra : 64 * RDS);
   return L;
 }
@@ -368,6 +383,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   cl[lane] = col;
   md[lane] = dist;
   __syncthreads();
+  int cnum = 0;
+  double cmin = 1e300;
   if (valid && i == 0) {
     int cls = 0, c = 0;
     double m = prm_of(a, sc)[DAT_P_VISR];
@@ -380,9 +397,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // longest scenarios are claimed first and scenarios sharing a wavefront tend to need similar
     // numbers of ADMM passes and of IPM iterations per pass (a pass lasts as long as its slowest lane)
     const int bin = NPB * iter_bin(a.iters[sc]) + ipm_bin(a.ipmx[sc]);
-    a.need[sc] = cls * NIB + (NIB - 1 - bin);
+    // a scenario wedged in a stall (previous step > TAIL_PREV passes) goes to the tail (key NKEY + class)
+    a.need[sc] = a.iters[sc] > a.tail_prev ? NKEY + cls : cls * NIB + (NIB - 1 - bin);
     a.col[sc] = (unsigned char)c;
     a.mind[sc] = m;
+    cnum = c;
+    cmin = m;
+  }
+  // collisions and the smallest env distance of the step (bench stats; one atomic per wavefront, the minimum only
+  // when it undercuts the running one)
+  for (int off = 32; off > 0; off >>= 1) {
+    cnum += __shfl_xor(cnum, off);
+    cmin = fmin(cmin, __shfl_xor(cmin, off));
+  }
+  if (lane == 0) {
+    if (cnum) atomicAdd(a.counters + CNT_COLL, (unsigned long long)cnum);
+    unsigned long long* pm = a.counters + CNT_COLL + 1;
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(cmin);
+    if (cmin >= 0.0 && bits < *(volatile unsigned long long*)pm) atomicMin(pm, bits);
   }
 }
 
@@ -395,21 +427,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 // scenarios share a wavefront, never a scenario's arithmetic (the capped-grid test compares two
 // different groupings bitwise).
 constexpr int BUCKET_T = 1024;
-static_assert(NKEY <= BUCKET_T, "k_bucket initialises one key per thread");
+static_assert(NKEY_ALL <= BUCKET_T, "k_bucket initialises one key per thread");
 __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int* list, int* count) {
-  __shared__ int hist[NKEY], kstart[NKEY], cursor[NKEY], tot[NKEY];
+  __shared__ int hist[NKEY_ALL], kstart[NKEY_ALL], cursor[NKEY_ALL], tot[NKEY_ALL];
   const int t = threadIdx.x;
-  if (t < NKEY) { hist[t] = 0; cursor[t] = 0; }
+  if (t < NKEY_ALL) { hist[t] = 0; cursor[t] = 0; }
   __syncthreads();
-  for (int q = t; q < B; q += BUCKET_T) atomicAdd(&hist[min(max(need[q], 0), NKEY - 1)], 1);
+  for (int q = t; q < B; q += BUCKET_T) atomicAdd(&hist[min(max(need[q], 0), NKEY_ALL - 1)], 1);
   __syncthreads();
   if (t == 0) {
     int st = 0;
-    for (int k = 0; k < NKEY; ++k) { kstart[k] = st; tot[k] = hist[k]; st += hist[k]; }
+    for (int k = 0; k < NKEY_ALL; ++k) { kstart[k] = st; tot[k] = hist[k]; st += hist[k]; }
   }
   __syncthreads();
   for (int q = t; q < B; q += BUCKET_T) {
-    const int key = min(max(need[q], 0), NKEY - 1);
+    const int key = min(max(need[q], 0), NKEY_ALL - 1);
     list[kstart[key] + atomicAdd(&cursor[key], 1)] = q;
   }
   if (t == 0) {
@@ -420,9 +452,14 @@ __global__ __launch_bounds__(BUCKET_T) void k_bucket(int B, const int* need, int
       count[cl] = sz;
       count[NCLS + cl] = st;
       count[2 * NCLS + cl] = 0;  // queue head of the class (k_cadmm)
-      count[3 * NCLS + cl] = 0;  // robust list of the class (k_cadmm -> k_cadmm_rob) and its head
+      count[3 * NCLS + cl] = 0;  // hand-over list of the class (k_cadmm -> k_cadmm_tail) and its head
       count[4 * NCLS + cl] = 0;
       st += sz;
+    }
+    for (int cl = 0; cl < NCLS; ++cl) {  // the tail-routed stretches (keys NKEY + class) behind them
+      count[5 * NCLS + cl] = tot[NKEY + cl];
+      count[6 * NCLS + cl] = kstart[NKEY + cl];
+      count[7 * NCLS + cl] = 0;
     }
   }
 }
@@ -433,6 +470,7 @@ struct WaveCounters {
   long long inband = 0, loose = 0;      // lane-level: solves accepted through the best in-band iterate
   long long refs = 0, corrs = 0;        // lane-level: IPM refinement passes, corrections applied
   long long slot = 0, pass = 0;         // wave-level: sum of (max lane IPM iterations) per pass, passes
+  long long cert = 0, stall = 0, warm = 0;  // k_cadmm_tail, lane-level: certified infeasible, stall exits, warm starts
 };
 
 // A persistent 64-lane block drains the queue of env class CLS (the class's stretch of the sorted
@@ -444,11 +482,16 @@ struct WaveCounters {
 // Every agent QP is solved as ipm_solve IPM_FAST_REDO defines it: the fast solver, redone by the robust one
 // when it does not end cleanly (ipm_unclean).  RB = false (k_cadmm) carries only the fast solver (IPM_FAST): a
 // scenario one of whose agent QPs does not end cleanly leaves at the end of that pass's solves with a resume
-// record (rres) and goes to its class's robust list.  RB = true (k_cadmm_rob, launched after k_cadmm) drains
-// the robust lists with IPM_FAST_REDO, resuming each scenario in the pass it left (re-solving there only the
-// agent QPs handed over) and finishing its step (and its later fused steps).  Built with -ffp-contract=on
-// (multiply-adds fused within an expression only), the inlined solver computes the same bits in either
-// kernel, so a scenario's results do not depend on which kernel ran which pass.
+// record (rres) and goes to its class's hand-over list; so does a scenario whose next pass falls under the tail
+// rule (TAIL_PREV / TAIL_PASS, dat_kargs.hpp), at the end of the pass before it.  RB = true (k_cadmm_tail: one
+// scenario slot per wavefront) drains the hand-over lists after k_cadmm (tmode 0), resuming each scenario in
+// the pass it left (re-solving there only the agent QPs handed over), or the scenarios k_env_class routed to the
+// tail before the step, concurrently with k_cadmm (tmode 1), and finishes their steps (and later fused steps).
+// The tail's solves: IPM_FAST_REDO with the certificate of infeasible rows (dvl_rows_infeasible, once per
+// scenario-step) and, in the passes the tail rule names, the warm start from the agent QP's converged iterate of
+// the previous pass and the stall exit (ipm_solve WS).  Built with -ffp-contract=on (multiply-adds fused within
+// an expression only), the inlined fast solver computes the same bits in either kernel, and the tail rule
+// depends on the scenario's own history: a scenario's results do not depend on which kernel ran which pass.
 template <int CLS, bool RB>
 __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr bool ENV = CLS > 0;
@@ -460,12 +503,13 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   const int lane = threadIdx.x;
   const int ls = lane / n, i = lane - ls * n;
   const int lsc = ls < G ? ls : 0;
-  const int first = a.scount[NCLS + CLS];
-  const int cnt = RB ? a.scount[3 * NCLS + CLS] : a.scount[CLS];
+  const bool TM = RB && a.tmode == 1;  // the tail-routed stretch of slist (k_env_class), not the hand-over list
+  const int first = TM ? a.scount[6 * NCLS + CLS] : a.scount[NCLS + CLS];
+  const int cnt = TM ? a.scount[5 * NCLS + CLS] : RB ? a.scount[3 * NCLS + CLS] : a.scount[CLS];
   if (cnt == 0) return;
-  int* const qh = RB ? a.scount + 4 * NCLS + CLS : a.qhead + CLS;
-  const int* const ql = (RB ? a.rlist : a.slist) + first;
-  const int rmode = cadmm_row_mode(n, G, CLS);  // wave-uniform
+  int* const qh = TM ? a.scount + 7 * NCLS + CLS : RB ? a.scount + 4 * NCLS + CLS : a.qhead + CLS;
+  const int* const ql = (RB && !TM ? a.rlist : a.slist) + first;
+  const int rmode = RB ? 3 : cadmm_row_mode(n, G, CLS);  // wave-uniform
   CadmmLds L = cadmm_carve(smem, n, G, CLS, rmode);
   double* fb = L.fbar + lsc * N3;
   double* rts = L.Rt + lsc * RT_STRIDE * n;
@@ -486,9 +530,10 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   double* cfs = nullptr;  // the scenario's n agent copies f^(j), in the warm-state array (HBM / L2)
   double* myf = nullptr;
   double* bst = nullptr;
+  double* wrl = nullptr;  // k_cadmm_tail: the lane's warm-start record
   int iter = 0, prev_iter = 0, qstat = ST_OPTIMAL;
   int kstep = 0;  // fused control steps (dat_control_steps): the slot scenario's current step
-  int rmask = -1;  // k_cadmm_rob: the lanes that solve in the current pass (a resumed pass: those handed over)
+  int rmask = -1;  // k_cadmm_tail: the lanes that solve in the current pass (a resumed pass: those handed over)
   double rho = a.rho0;
   WaveCounters wc;
   for (;;) {
@@ -503,7 +548,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }
       L.sid[ls] = s2;
       L.done[ls] = 0;
-      L.wmx[ls] = RB && s2 >= 0 ? a.rres[(size_t)s2 * RRES_INTS + RRES_WMX] : 0;
+      L.wmx[ls] = RB && !TM && s2 >= 0 ? a.rres[(size_t)s2 * RRES_INTS + RRES_WMX] : 0;
     }
     __syncthreads();
     const int slot_sc = lane < NT ? L.sid[ls] : -2;
@@ -525,6 +570,10 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       kstep = 0;
       rmask = -1;
       if (RB) {
+        wrl = a.wrec + ((size_t)sc * n + i) * WREC_SIZE;
+        wrl[0] = 0.0;  // no recorded iterate yet
+      }
+      if (RB && !TM) {
         // where k_cadmm left the scenario (its warm state -- multipliers, copies, the mean -- is in place)
         const int* const rr = a.rres + (size_t)sc * RRES_INTS;
         kstep = rr[RRES_KSTEP];
@@ -556,6 +605,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         EnvRows E;
         set_env_rows(P, E, S, emask, lhs, rhs);
         env_to_lds<NE>(L.env, lane, E);
+        // the tail certifies infeasible rows once per scenario-step (such an agent QP would run 2 x 50 IPM
+        // iterations in every pass and end INACCURATE: the previous solution is held either way)
+        if (RB && !P.infeasible && dvl_rows_infeasible(shr, err, P.emask)) {
+          P.infeasible = 1;
+          ++wc.cert;
+        }
       }
     }
     // ---- one ADMM pass of every occupied slot
@@ -574,7 +629,15 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       constexpr int RM = RB ? IPM_FAST_REDO : IPM_FAST;
       using SHT = LdsRef<QPShared>;
       using ERT = EnvLdsN<NE>;
-      if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
+      if constexpr (RB) {
+        // the tail rule: warm start and stall exit in pass iter (the record is kept in every pass)
+        const bool wson = iter >= 1 && (prev_iter > a.tail_prev || iter >= a.tail_pass);
+        wc.warm += wson && wrl[0] == 1.0;
+        o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, TAIL_AUXM, NoGrp, RM, true>(
+            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane},
+            NoGrp{}, wrl, wson);
+        wc.stall += o.why == 7;
+      } else if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
         if (AUXM != 0 && rmode == 2)
           o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, AUXM, NoGrp, RM>(
               shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane});
@@ -590,9 +653,9 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }
       hand = !RB && ipm_unclean(o);
       DAT_PHASE(9);
-      // a solve k_cadmm hands over is counted once, by k_cadmm_rob (its IPM_FAST_REDO runs the fast attempt
+      // a solve k_cadmm hands over is counted once, by k_cadmm_tail (its IPM_FAST_REDO runs the fast attempt
       // again): its discarded outcome here is neither an agent-QP solve nor an in-band accept
-      const int keep = hand ? 0 : 1;
+      const int keep = hand ? 0 : 1;  // (nor do its iterations enter the pass's slot counts)
       wc.ipm += keep * o.iters;
       wc.inband += keep * o.inband;
 #ifdef DAT_ITER_HIST
@@ -601,7 +664,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       wc.loose += keep * inband_loose(o);
       wc.refs += keep * o.refs;
       wc.corrs += keep * o.corrs;
-      it_lane = o.iters;
+      it_lane = keep * o.iters;
       wc.rowit += (long long)(keep * o.iters) * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       wc.qp += keep;
       qstat = o.status;
@@ -618,7 +681,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }  // otherwise hold the previous solution (control/rqp_cadmm.py:496-499)
     }
     DAT_PHASE(13);
-    wc.slot += wave_max(it_lane);
+    wc.slot += wave_max(it_lane);  // (the tail's passes: counted apart, CNT_TAIL)
     ++wc.pass;
     if (active) atomicMax(&L.wmx[ls], it_lane);
     rmask = -1;
@@ -627,7 +690,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     const int hmask = lane < NT ? (int)((hb >> (ls * n)) & ((1ull << n) - 1ull)) : 0;
     __syncthreads();
     if (!RB && active && hmask) {
-      // an agent QP of the pass was not clean: k_cadmm_rob resumes the scenario here (the mean of the pass's
+      // an agent QP of the pass was not clean: k_cadmm_tail resumes the scenario here (the mean of the pass's
       // start, the statuses of the pass's other solves; multipliers and copies are in place)
       for (int c = 0; c < 3; ++c) a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
       a.qstatus[(size_t)sc * n + i] = qstat;
@@ -716,9 +779,27 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     if (active) {
       if (!L.done[ls]) {
         for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
+        if (!RB && iter >= 1 && (prev_iter > a.tail_prev || iter >= a.tail_pass)) {
+          // the tail rule holds from the next pass on: k_cadmm_tail resumes the scenario there (all lanes solve;
+          // the mean of this pass goes with it, multipliers and copies are in place)
+          for (int c = 0; c < 3; ++c) a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
+          a.qstatus[(size_t)sc * n + i] = qstat;
+          if (i == 0) {
+            int* const rr = a.rres + (size_t)sc * RRES_INTS;
+            rr[RRES_KSTEP] = kstep;
+            rr[RRES_PASS] = iter;
+            rr[RRES_WMX] = L.wmx[ls];
+            rr[RRES_LANES] = -1;
+            a.rlist[first + atomicAdd(a.scount + 3 * NCLS + CLS, 1)] = sc;
+            L.sid[ls] = -1;
+          }
+        }
       } else {
         // the scenario stopped: write its outputs and free the slot
-        if (RB && i == 0) atomicAdd(a.counters + CNT_ROB, 1ull);
+        if (RB && i == 0) {  // a scenario-step the tail finished (and, routed before the step, counted apart)
+          atomicAdd(a.counters + CNT_ROB, 1ull);
+          if (TM && kstep == 0) atomicAdd(a.counters + CNT_TAIL + 2, 1ull);
+        }
         for (int c = 0; c < 3; ++c) {
           a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
           a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
@@ -736,6 +817,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           iter = 0;
           qstat = ST_OPTIMAL;
           rho = a.rho0;
+          if (RB) wrl[0] = 0.0;
           if (i == 0) {
             build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
                          prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
@@ -752,6 +834,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   unsigned long long q = (unsigned long long)wc.qp, ip = (unsigned long long)wc.ipm, rw = (unsigned long long)wc.rowit;
   unsigned long long ib = (unsigned long long)wc.inband, lo = (unsigned long long)wc.loose;
   unsigned long long rf = (unsigned long long)wc.refs, co = (unsigned long long)wc.corrs;
+  unsigned long long ce = (unsigned long long)wc.cert, sx = (unsigned long long)wc.stall, wm = (unsigned long long)wc.warm;
   for (int off = 32; off > 0; off >>= 1) {
     q += __shfl_xor(q, off);
     ip += __shfl_xor(ip, off);
@@ -760,14 +843,28 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     lo += __shfl_xor(lo, off);
     rf += __shfl_xor(rf, off);
     co += __shfl_xor(co, off);
+    if (RB) {
+      ce += __shfl_xor(ce, off);
+      sx += __shfl_xor(sx, off);
+      wm += __shfl_xor(wm, off);
+    }
   }
   if (lane == 0) {
     unsigned long long* cc = a.counters + CNT_STRIDE * CLS;
     atomicAdd(cc, q);
     atomicAdd(cc + 1, ip);
     atomicAdd(cc + 2, rw);
-    atomicAdd(cc + 3, (unsigned long long)(wc.slot * NT));
-    atomicAdd(cc + 4, (unsigned long long)(wc.pass * G));
+    if (RB) {  // the tail's occupancy apart from k_cadmm's class counters
+      unsigned long long* ct = a.counters + CNT_TAIL;
+      atomicAdd(ct, (unsigned long long)wc.pass);
+      atomicAdd(ct + 1, (unsigned long long)wc.slot);
+      if (ce) atomicAdd(ct + 3, ce);
+      if (sx) atomicAdd(ct + 4, sx);
+      if (wm) atomicAdd(ct + 5, wm);
+    } else {
+      atomicAdd(cc + 3, (unsigned long long)(wc.slot * NT));
+      atomicAdd(cc + 4, (unsigned long long)(wc.pass * G));
+    }
     if (ib) atomicAdd(a.counters + CNT_INBAND, ib);
     if (lo) atomicAdd(a.counters + CNT_INBAND + 1, lo);
     atomicAdd(a.counters + CNT_REF, rf);
@@ -787,10 +884,12 @@ __global__ __launch_bounds__(64) void k_cadmm(KArgs a) {
   cadmm_drain<1, false>(a);
   cadmm_drain<0, false>(a);
 }
-// The steps k_cadmm handed over (an agent QP not clean), finished with the robust redo: a kernel of its own,
-// because the robust solver compiled into k_cadmm cost the fast path 36-60 % (register allocation, C4 A/B).
-// Launched after every k_cadmm; without a listed scenario its blocks return at once.
-__global__ __launch_bounds__(64) void k_cadmm_rob(KArgs a) {
+// The tail: the scenario-steps k_cadmm handed over (an agent QP not clean, or the tail rule) and, launched
+// concurrently with k_cadmm, those k_env_class routed here (wedged in a stall), one scenario per wavefront,
+// every class's row state and IPM aux slots in LDS: the robust redo, the certificate of infeasible rows, the warm
+// start and stall exit of the tail rule's passes.  A kernel of its own: the robust solver compiled into k_cadmm
+// cost the fast path 36-60 % (register allocation, C4 A/B).  Without a listed scenario its blocks return at once.
+__global__ __launch_bounds__(64) void k_cadmm_tail(KArgs a) {
   cadmm_drain<3, true>(a);
   cadmm_drain<2, true>(a);
   cadmm_drain<1, true>(a);
@@ -802,7 +901,7 @@ __global__ __launch_bounds__(64) void k_cadmm_rob(KArgs a) {
 // With a forest one launch per class measured 2x slower on C4 (each class launch drains to its own
 // tail): k_cadmm keeps the four drains in one launch there.
 __global__ __launch_bounds__(64) void k_cadmm0(KArgs a) { cadmm_drain<0, false>(a); }
-__global__ __launch_bounds__(64) void k_cadmm0_rob(KArgs a) { cadmm_drain<0, true>(a); }
+__global__ __launch_bounds__(64) void k_cadmm0_tail(KArgs a) { cadmm_drain<0, true>(a); }
 
 // ------------------------------------------------------------------------------------------------
 // DD: quasi-Newton matrix inverse per scenario (one 64-lane block per scenario)
@@ -1684,6 +1783,8 @@ __global__ __launch_bounds__(64) void k_agent_qp(KArgs a, AgentQPArgs q) {
   const EnvPlain er{&E};
   const RtPtr rtr{Rt_all + 9 * i};
   double* bst = q.best + (size_t)k * best_size(1);
+  // the C-ADMM agent QP as the closed loop solves it: rows certified infeasible are held (k_cadmm_tail)
+  if (!dd && !P.infeasible && dvl_rows_infeasible(shr, er, P.emask)) P.infeasible = 1;
   IPMOut o = dd ? ipm_solve_rows<MODE_DD, 1>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER,
                                              a.qp_tol)
                 : ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(nr, shr, er, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst,
@@ -1767,6 +1868,10 @@ struct dat_handle {
   hipStream_t sub_stream[DAT_MAX_SUB] = {};
   hipEvent_t sub_done[DAT_MAX_SUB] = {};
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
+  // C-ADMM with a forest: per sub-batch the stream of the concurrent tail launch and its start / end events
+  hipStream_t tail_stream[DAT_MAX_SUB] = {};
+  hipEvent_t tail_ev[2 * DAT_MAX_SUB] = {};
+  double* wrec = nullptr;  // C-ADMM: the tail's warm-start records (B n WREC_SIZE)
   double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
   std::vector<void*> allocs;
@@ -1857,6 +1962,10 @@ KArgs kargs(dat_handle* h) {
   a.rlist = h->rlist;
   a.rres = h->rres;
   a.ll_kind = h->ll_kind;
+  a.wrec = h->wrec;
+  a.tail_prev = h->nforest > 0 ? TAIL_PREV : INT_MAX;
+  a.tail_pass = h->nforest > 0 ? TAIL_PASS : INT_MAX;
+  a.tmode = 0;
   return a;
 }
 
@@ -1871,21 +1980,32 @@ size_t dd_setup_lds(int n) {
   return sizeof(double) * (81 * (size_t)n + 9 * (size_t)n + dd_setup_hs(n) + N);
 }
 
-// the C-ADMM drain of one control step: k_cadmm (env classes 3, 2, 1, 0) with a forest, k_cadmm0 without
-// k_cadmm_rob: blocks of the robust redo, one scenario slot each (G = 1).  The listed scenarios are few --
-// stalled ADMM loops next to trees, 101 sequential passes -- and run after k_cadmm: a slot of its own per
-// scenario keeps one scenario's pass from waiting for the slowest agent QP of the others'.
-constexpr int ROB_BLOCKS = 256;
-void launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st) {
+// the C-ADMM drain of one control step: k_cadmm (env classes 3, 2, 1, 0) with a forest, k_cadmm0 without.
+// k_cadmm_tail: one scenario slot per block (G = 1).  Its scenarios are few -- stalled ADMM loops next to trees,
+// 101 sequential passes -- and a slot of its own per scenario keeps one scenario's pass from waiting for the
+// slowest agent QP of the others'.  With a forest two launches: the tail-routed scenarios on the sub-batch's
+// tail stream, started with k_cadmm (their lists are known after k_bucket), and the hand-over lists after
+// k_cadmm on the step's stream, which then waits for the first.
+constexpr int TAIL_BLOCKS = 256;
+int launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st, int sub = 0) {
   KArgs r = a;
   r.G = 1;
   if (h->nforest > 0) {
+    KArgs t = r;
+    t.tmode = 1;
+    const hipStream_t ts = h->tail_stream[sub];
+    HIPCHK(hipEventRecord(h->tail_ev[2 * sub], st));
+    HIPCHK(hipStreamWaitEvent(ts, h->tail_ev[2 * sub], 0));
+    hipLaunchKernelGGL(k_cadmm_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(a.n, NCLS - 1), ts, t);
+    HIPCHK(hipEventRecord(h->tail_ev[2 * sub + 1], ts));
     hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
-    hipLaunchKernelGGL(k_cadmm_rob, dim3(ROB_BLOCKS), dim3(64), cadmm_lds_bytes(r.n, r.G, NCLS - 1), st, r);
+    hipLaunchKernelGGL(k_cadmm_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(r.n, NCLS - 1), st, r);
+    HIPCHK(hipStreamWaitEvent(st, h->tail_ev[2 * sub + 1], 0));
   } else {
     hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
-    hipLaunchKernelGGL(k_cadmm0_rob, dim3(ROB_BLOCKS), dim3(64), cadmm_lds_bytes(r.n, r.G, 0), st, r);
+    hipLaunchKernelGGL(k_cadmm0_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(r.n, 0), st, r);
   }
+  return 0;
 }
 
 // ksteps > 1 (dat_control_steps): that many control steps fused into one drain, acc_seq ksteps x B x 6
@@ -1905,7 +2025,7 @@ int launch_hl(dat_handle* h, int ksteps = 1, const double* acc_seq = nullptr) {
     hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, h->stream, B, (const int*)h->need, h->slist, h->scount);
     HIPCHK(hipEventRecord(h->ek, h->stream));
     const int Gc = a.G, cblocks = (B + Gc - 1) / Gc;
-    launch_cadmm(h, a, std::min(cblocks, h->persistent_blocks), h->stream);
+    if (launch_cadmm(h, a, std::min(cblocks, h->persistent_blocks), h->stream)) return -1;
   } else if (h->cfg.mode == DAT_MODE_DD) {
     if (n > DD_REG_NMAX)  // [H | I] in LDS: beyond the default 64 KB dynamic LDS from n = 11 on
       HIPCHK(hipFuncSetAttribute((const void*)k_dd_setup<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1966,6 +2086,7 @@ KArgs sub_kargs(dat_handle* h, int off, int Bs, int s) {
   a.slist += o;
   a.rlist += o;
   a.rres += o * RRES_INTS;
+  a.wrec += o * n * WREC_SIZE;
   a.scount = h->scount + SCOUNT_INTS * s;
   a.qhead = a.scount + 2 * NCLS;
   a.erows += (size_t)4 * DAT_NENV * n * o;
@@ -2087,6 +2208,12 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->clam, B * n * N3);
     rc |= dalloc(h, &h->rres, B * RRES_INTS);
     rc |= dalloc(h, &h->rlist, B);
+    rc |= dalloc(h, &h->wrec, B * n * WREC_SIZE);
+    for (int s = 0; s < DAT_MAX_SUB && rc == 0; ++s)
+      if (hipStreamCreateWithFlags(&h->tail_stream[s], hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&h->tail_ev[2 * s], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&h->tail_ev[2 * s + 1], hipEventDisableTiming) != hipSuccess)
+        rc = fail("dat_create: tail stream/event creation failed");
   } else if (c.mode == DAT_MODE_DD) {
     rc |= dalloc(h, &h->need, B);
     rc |= dalloc(h, &h->ipmx, B);
@@ -2103,6 +2230,11 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
   // best-iterate records: one per agent QP lane (centralized: one per lane of the scenario's 16-lane slot)
   rc |= dalloc(h, &h->best, c.mode == DAT_MODE_CENTRALIZED ? B * 16 * (size_t)best_size(1) : B * n * (size_t)best_size(1));
   if (rc) {
+    std::string m = g_err;
+    dat_destroy(h);
+    return fail(m);
+  }
+  if (dat_reset_counters(h)) {
     std::string m = g_err;
     dat_destroy(h);
     return fail(m);
@@ -2127,6 +2259,14 @@ int dat_destroy(dat_handle* h) {
   for (int s = 1; s < DAT_MAX_SUB; ++s) {
     if (h->sub_stream[s]) (void)hipStreamDestroy(h->sub_stream[s]);
     if (h->sub_done[s]) (void)hipEventDestroy(h->sub_done[s]);
+  }
+  for (int s = 0; s < DAT_MAX_SUB; ++s) {
+    if (h->tail_stream[s]) {
+      (void)hipStreamSynchronize(h->tail_stream[s]);
+      (void)hipStreamDestroy(h->tail_stream[s]);
+    }
+    if (h->tail_ev[2 * s]) (void)hipEventDestroy(h->tail_ev[2 * s]);
+    if (h->tail_ev[2 * s + 1]) (void)hipEventDestroy(h->tail_ev[2 * s + 1]);
   }
   if (h->ev_start) (void)hipEventDestroy(h->ev_start);
   if (h->ev_end) (void)hipEventDestroy(h->ev_end);
@@ -2361,7 +2501,7 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
       hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, st, Bs, (const int*)a.need, a.slist, a.scount);
       const hipEvent_t* ev = h->sub_ev.data() + 2 * ((size_t)k * S + s);
       HIPCHK(hipEventRecord(ev[0], st));
-      launch_cadmm(h, a, std::min((Bs + a.G - 1) / a.G, h->persistent_blocks), st);
+      if (launch_cadmm(h, a, std::min((Bs + a.G - 1) / a.G, h->persistent_blocks), st, s)) return -1;
       HIPCHK(hipEventRecord(ev[1], st));
       launch_rollout(a, Bs, st, h->cfg.hl_every, h->cfg.dt, (const double*)a.fdes);
       HIPCHK(hipGetLastError());
@@ -2487,6 +2627,10 @@ int dat_reset_counters(dat_handle* h) {
   if (!h) return fail("null handle");
   HIPCHK(hipSetDevice(h->cfg.device));
   HIPCHK(hipMemsetAsync(h->counters, 0, DAT_NCOUNTERS * sizeof(unsigned long long), h->stream));
+  {  // the running minimum of the env distance starts at +inf
+    static const double inf = HUGE_VAL;
+    HIPCHK(hipMemcpyAsync(h->counters + CNT_COLL + 1, &inf, sizeof(inf), hipMemcpyHostToDevice, h->stream));
+  }
   h->cadmm_ms = 0.0;
   HIPCHK(hipStreamSynchronize(h->stream));
   h->hl_steps = 0;
@@ -2688,6 +2832,31 @@ int dat_get_robust_redos(dat_handle* h, long long* redos) {
   HIPCHK(hipMemcpyAsync(&c, h->counters + CNT_ROB, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (redos) *redos = (long long)c;
+  return 0;
+}
+
+int dat_get_tail_counters(dat_handle* h, long long* out) {
+  if (!h || !out) return fail("dat_get_tail_counters: null argument");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[6] = {};
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_TAIL, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < 6; ++k) out[k] = (long long)c[k];
+  return 0;
+}
+
+int dat_get_collision_stats(dat_handle* h, long long* collisions, double* min_env_dist) {
+  if (!h) return fail("dat_get_collision_stats: null handle");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  unsigned long long c[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(c, h->counters + CNT_COLL, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (collisions) *collisions = (long long)c[0];
+  if (min_env_dist) {
+    double m;
+    memcpy(&m, &c[1], sizeof(m));
+    *min_env_dist = m;
+  }
   return 0;
 }
 

@@ -29,22 +29,37 @@ __host__ __device__ inline int iter_bin(int it) {
 // IPM iterations of a scenario's slowest agent QP: <= 4, 5, 6-7, >= 8 (six bins measured no gain, round 3)
 __host__ __device__ inline int ipm_bin(int it) { return it <= 4 ? 0 : it == 5 ? 1 : it <= 7 ? 2 : 3; }
 constexpr int NKEY = NCLS * NIB;
+// C-ADMM with a forest, the tail rule (TAIL_PREV, TAIL_PASS: dat_qp.hpp).  k_env_class routes the scenarios
+// whose previous step took more than TAIL_PREV passes before the step (sort keys NKEY + class: the tail list
+// drained concurrently with k_cadmm); k_cadmm hands a scenario over at the end of the pass after which the rule
+// holds (resume record, the hand-over list drained after k_cadmm).
+constexpr int NKEY_ALL = NKEY + NCLS;
 constexpr int CNT_STRIDE = 5;  // per class: QP solves, IPM iterations, x rows, slot iterations, wave passes
 // QPs accepted through the best in-band iterate of a stalled IPM (all kernels), and those of them whose
 // scaled residual / gap exceeds Clarabel's own tolerance (INBAND_CLARABEL)
 constexpr int CNT_INBAND = NCLS * CNT_STRIDE;
 // IPM refinement passes run and corrections applied (all kernels; the executed-flop model)
 constexpr int CNT_REF = CNT_INBAND + 2;
-// C-ADMM control steps of a scenario finished by k_cadmm_rob (an agent QP not clean in k_cadmm, ipm_unclean)
+// C-ADMM control steps of a scenario finished by k_cadmm_tail (handed over by k_cadmm: an agent QP not clean,
+// ipm_unclean, or the tail rule; or routed there before the step)
 constexpr int CNT_ROB = CNT_REF + 2;
-constexpr int DAT_NCOUNTERS = CNT_ROB + 1;
+// tail kernel: [0] ADMM passes (wavefront), [1] sum over passes of the slowest agent QP's IPM iterations,
+// [2] scenario-steps routed before the step, [3] agent QPs whose rows were certified infeasible
+// (dvl_rows_infeasible, per scenario-step), [4] stall exits, [5] warm-started solves
+constexpr int CNT_TAIL = CNT_ROB + 1;
+// k_env_class: [0] scenario-steps with a collision flag (example/env_forest.py:158-159), [1] the smallest
+// min env distance of the counted steps (fp64 bits: atomicMin orders positive doubles)
+constexpr int CNT_COLL = CNT_TAIL + 6;
+constexpr int DAT_NCOUNTERS = CNT_COLL + 2;
 // class table of the C-ADMM / DD queues (k_bucket), per sub-batch: [0, NCLS) class sizes, [NCLS, 2 NCLS) class
 // starts in slist, [2 NCLS, 3 NCLS) queue heads; C-ADMM robust redo: [3 NCLS, 4 NCLS) sizes of the classes'
 // robust lists (rlist, same class starts), [4 NCLS, 5 NCLS) their queue heads
-constexpr int SCOUNT_INTS = 5 * NCLS;
+// [5 NCLS, 6 NCLS) sizes of the classes' tail-routed stretches of slist (keys NKEY + class), [6 NCLS, 7 NCLS)
+// their starts, [7 NCLS, 8 NCLS) their heads
+constexpr int SCOUNT_INTS = 8 * NCLS;
 // Resume record of a scenario k_cadmm hands to k_cadmm_rob: the fused control step and the ADMM pass it
 // stopped in, the IPM-iteration maximum so far, and the mask of its agent lanes whose solve of that pass
-// was not clean (the others' results of the pass stand)
+// was not clean (the others' results of the pass stand; -1: all, a hand-over between passes by the tail rule)
 constexpr int RRES_KSTEP = 0, RRES_PASS = 1, RRES_WMX = 2, RRES_LANES = 3, RRES_INTS = 4;
 constexpr double INBAND_CLARABEL = IPM_CLARABEL_TOL;
 __device__ inline int inband_loose(const IPMOut& o) { return o.inband && o.merit > INBAND_CLARABEL; }
@@ -92,6 +107,9 @@ struct KArgs {
   double qp_tol;                 // IPM stopping tolerance of every QP (dat_set_qp_tolerance)
   int ksteps;                    // C-ADMM / DD without a forest: control steps fused into one drain
                                  // (dat_control_steps; acc then holds ksteps x B x 6 values)
+  double* wrec;                  // C-ADMM tail: per agent lane the warm-start record (WREC_SIZE doubles)
+  int tail_prev, tail_pass;      // C-ADMM: the tail rule (TAIL_PREV / TAIL_PASS with a forest, INT_MAX without)
+  int tmode;                     // k_cadmm_tail: 0 the hand-over lists (rlist), 1 the tail-routed stretch of slist
 };
 
 // wave-uniform maximum (every lane of the wavefront must execute it)

@@ -173,7 +173,7 @@ DAT_HD int rows_needed(unsigned emask) { return NBASE + (emask ? 32 - __builtin_
 // Stiff rows: a row slot whose barrier weight z/s exceeds IPM_STIFF_W is kept out of the normal-equation
 // matrix M and solved in augmented (quasi-definite) form, at most IPM_NSTIFF per solve (see ipm_attempt)
 constexpr double IPM_STIFF_W = 1e12;
-constexpr int IPM_NSTIFF = 4;
+constexpr int IPM_NSTIFF = 8;
 
 // size (doubles) of the lane-private best-iterate record: y (3 NB), w (6), pi (6), u (6) (best_rec: all a
 // non-robust instantiation touches, the stride k_cadmm, DD and centralized index with) plus, behind it, the
@@ -188,6 +188,27 @@ DAT_HD constexpr int best_size(int NB) {
 }
 // Clarabel's own tolerance: an in-band exit whose merit is above it is one Clarabel would not certify
 constexpr double IPM_CLARABEL_TOL = 1e-8;
+
+// Warm start (start 3, ipm_solve WS): the previous ADMM pass's converged iterate of the same agent QP, in a
+// lane record of WREC_SIZE doubles -- [0] valid flag, y (3), w (6), cone slacks (9) and duals (9), the row
+// slacks and duals (DAT_MAXROW each) -- pushed back into the interior so that every complementarity pair's
+// product is at least WS_MU (a pair (s, z) below it moves to (s + d, z + d); a second-order cone pair by its
+// margins s0 - |s1:3|, z0 - |z1:3|).  The attempt is capped at WS_MAXIT iterations; one that does not converge
+// cleanly goes on to the cold starts.
+constexpr double WS_MU = 1e2;
+constexpr int WS_MAXIT = 30;
+// stall exit of the tail kernel's solves (ipm_attempt WS): best in-band merit <= WS_STALL_TOL and not halved
+// in WS_STALL_ITS iterations
+constexpr double WS_STALL_TOL = 1e-9;
+constexpr int WS_STALL_ITS = 3;
+constexpr int WREC_SIZE = 28 + 2 * DAT_MAXROW;
+// The tail rule of the C-ADMM closed loop with a forest: ADMM pass p of a scenario's control step solves its
+// agent QPs with the warm start and the stall exit exactly when p >= 1 and (the scenario's previous step took more
+// than TAIL_PREV passes -- it is wedged in a stall, where every step is the reference loop's 101-pass max_iter
+// stall, control/rqp_cadmm.py:661 -- or p >= TAIL_PASS).  The GPU runs those passes in k_cadmm_tail (dat.hip).
+// The rule depends on the scenario's own history only, so its results do not depend on the scenarios it is
+// batched with.  Normal C4 steps take 1-14 passes: the warm closed loop never meets it.
+constexpr int TAIL_PREV = 20, TAIL_PASS = 16;
 
 // ------------------------------------------------------------------ shared data
 // k_f, k_m: total force / moment weights; variants: bit 0 build C[0] (kdv = 0), bit 1 build C[1]
@@ -317,7 +338,9 @@ DAT_HD void set_env_rows(QPLane<NB>& P, EnvRows& E, const QPShared& S, unsigned 
 #pragma unroll
   for (int j = 0; j < DAT_NENV; ++j) {
     const bool on = (mask >> j) & 1u;
-    const bool zero = lhs[j][0] == 0.0 && lhs[j][1] == 0.0 && lhs[j][2] == 0.0;
+    // a row whose coefficients vanish against its constant (|lhs| <= 1e-12 |rhs|: a rounding remnant, it would
+    // need accelerations beyond 1e12 to bind) is a zero row
+    const bool zero = lhs[j][0] * lhs[j][0] + lhs[j][1] * lhs[j][1] + lhs[j][2] * lhs[j][2] <= 1e-24 * rhs[j] * rhs[j];
     if (on && zero && -rhs[j] < 0.0) P.infeasible = 1;
     if (!on || zero) continue;
     const double bj = -rhs[j] + dot3(lhs[j], S.bv);
@@ -331,6 +354,96 @@ DAT_HD void set_env_rows(QPLane<NB>& P, EnvRows& E, const QPShared& S, unsigned 
     ++k;
   }
   P.emask = (1u << k) - 1u;
+}
+
+// Certified infeasibility of an agent QP's dvl rows (the |vl| base row, slot 2, and the env rows): a . x + b >= 0
+// with x = lin_v(u) in R^3.  In the C-ADMM (and DD) agent QP the aggregate w is free, so u is free and the QP is
+// infeasible exactly when its row system is (the cone block alone is feasible; the two dwl rows act on another
+// coordinate of u).  By Helly's theorem an empty intersection of half-spaces in R^3 has an empty subsystem of at
+// most 4 rows, and one of at most 3 when their normals lie in a plane (the env rows of vertical trees are
+// horizontal): a Farkas certificate lambda >= 0, sum_m lambda_m a_m = 0, sum_m lambda_m b_m < 0, with lambda the
+// signed cofactors of the subsystem -- two antiparallel normals, three coplanar ones (scalar cross products in
+// their plane) or four that positively span R^3 (3 x 3 determinants).  Only strict certificates count: lambda of
+// one sign with every entry above 1e-9 of their sum, and a violation beyond 1e-6 of the rows' scale; anything
+// closer is left to the IPM, so a certified QP is one whose residuals the IPM cannot bring into band either, and
+// one Clarabel reports infeasible (the reference then holds the previous solution, control/rqp_cadmm.py:496-499).
+// At most C(11, 2) + C(11, 3) + C(11, 4) = 550 subsystems: the tail kernel runs it once per scenario and step
+// (an infeasible agent QP otherwise runs 2 x 50 IPM iterations in every ADMM pass of a stall).
+template <class SH, class ER>
+DAT_HD bool dvl_rows_infeasible(const SH& sh, const ER& er, unsigned emask) {
+  const int ne = __builtin_popcount(emask);  // active env rows: slots 0 .. ne - 1 (set_env_rows compacts them)
+  const bool vrow = (sh.get().bmask >> 2) & 1;
+  const int m = ne + (vrow ? 1 : 0);
+  auto row = [&](int k, double* a, double& b) {
+    if (vrow && k == ne) {
+      double r4[4];
+      ldn<4>(sh.get().rows[2], r4);
+      a[0] = r4[0]; a[1] = r4[1]; a[2] = r4[2];
+      b = r4[3];
+    } else {
+      er.ab(k, a, b);
+    }
+  };
+  auto nrm = [](const double* a) { return sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); };
+  // lambda (of one sign, normalised positive) certifies infeasibility
+  auto cert = [](int q, const double* lam, const double* bb, const double* na) -> bool {
+    double sg = lam[0] < 0.0 ? -1.0 : 1.0, tot = 0.0;
+    for (int t = 0; t < q; ++t) tot += fabs(lam[t]);
+    double lb = 0.0, sc = 0.0;
+    for (int t = 0; t < q; ++t) {
+      const double l = sg * lam[t];
+      if (!(l > 1e-9 * tot)) return false;
+      lb += l * bb[t];
+      sc += l * (fabs(bb[t]) + na[t]);
+    }
+    return lb < -1e-6 * sc;
+  };
+  bool inf = false;
+#pragma unroll 1
+  for (int i = 0; i < m - 1; ++i) {
+    double a1[3], b1;
+    row(i, a1, b1);
+    const double n1 = nrm(a1);
+#pragma unroll 1
+    for (int j = i + 1; j < m; ++j) {
+      double a2[3], b2, c12[3];
+      row(j, a2, b2);
+      const double n2 = nrm(a2);
+      cross3(a1, a2, c12);
+      const double nc12 = nrm(c12);
+      if (nc12 <= 1e-9 * n1 * n2 && dot3(a1, a2) < 0.0) {  // antiparallel pair
+        const double lam[2] = {n2, n1}, bb[2] = {b1, b2}, na[2] = {n1, n2};
+        inf = inf || cert(2, lam, bb, na);
+      }
+#pragma unroll 1
+      for (int k = j + 1; k < m; ++k) {
+        double a3[3], b3, c23[3], c31[3];
+        row(k, a3, b3);
+        const double n3 = nrm(a3);
+        cross3(a2, a3, c23);
+        cross3(a3, a1, c31);
+        const double l4 = -dot3(c12, a3);  // -det(a1, a2, a3)
+        if (fabs(l4) <= 1e-9 * n1 * n2 * n3) {  // coplanar triple: scalar cross products in the plane
+          const double* nv = c12;
+          if (nrm(c23) > nrm(nv)) nv = c23;
+          if (nrm(c31) > nrm(nv)) nv = c31;
+          const double lam[3] = {dot3(nv, c23), dot3(nv, c31), dot3(nv, c12)}, bb[3] = {b1, b2, b3},
+                       na[3] = {n1, n2, n3};
+          inf = inf || cert(3, lam, bb, na);
+        }
+#pragma unroll 1
+        for (int l = k + 1; l < m; ++l) {
+          double a4[3], b4, c34[3];
+          row(l, a4, b4);
+          cross3(a3, a4, c34);
+          const double lam[4] = {dot3(a2, c34), -dot3(a1, c34), dot3(c12, a4), l4}, bb[4] = {b1, b2, b3, b4},
+                       na[4] = {n1, n2, n3, nrm(a4)};
+          inf = inf || cert(4, lam, bb, na);
+        }
+      }
+    }
+  }
+  return inf;
 }
 
 // ------------------------------------------------------------------ per-agent data
@@ -707,11 +820,12 @@ struct IPMOut {
 // adds exactly nothing); row reciprocals, primal residuals and the corrector's second-order row
 // terms are recomputed where consumed instead of being kept live.
 // ROB: the robust instantiation (stiff rows in augmented form, below).
-template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB>
+template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsigned AUXM, class GRP, bool ROB,
+          bool WS = false>
 DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
                                                           const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
-                          int start) {
+                          int start, double* wrec = nullptr, bool wson = false) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   // aux slot offsets (only the AUXM groups are allocated)
   constexpr int O_SC = 0;
@@ -960,6 +1074,53 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
 #pragma unroll
     for (int l = 0; l < NR; ++l) SL(l) = fmax(rowval(l, dv, dw), S0);
   }
+  if constexpr (WS) {
+    static_assert(NB == 1 && NR <= DAT_MAXROW, "warm start: C-ADMM agent QP");
+    if (start == 3) {
+      // (s, z) -> (s + d, z + d) with (s + d)(z + d) >= WS_MU
+      auto push = [](double s, double z) -> double {
+        const double p = s * z;
+        if (!(p < WS_MU)) return 0.0;
+        const double t = s + z;
+        return 0.5 * (sqrt(t * t + 4.0 * (WS_MU - p)) - t);
+      };
+#pragma unroll
+      for (int c = 0; c < 3; ++c) y[0][c] = wrec[1 + c];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) w[r] = wrec[4 + r];
+      double g[9];
+      Gy(y[0], g);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        sk[0][j] = -g[j];
+        zk[0][j] = wrec[19 + j];
+      }
+      sk[0][0] -= mfz;
+      sk[0][5] += mxf;
+      {
+        const double d = push(fmax(sk[0][0], 0.0), fmax(zk[0][0], 0.0));
+        sk[0][0] = fmax(sk[0][0], 0.0) + d;
+        zk[0][0] = fmax(zk[0][0], 0.0) + d;
+      }
+#pragma unroll
+      for (int b = 1; b <= 5; b += 4) {
+        const double ms = sk[0][b] - sqrt(sk[0][b + 1] * sk[0][b + 1] + sk[0][b + 2] * sk[0][b + 2] + sk[0][b + 3] * sk[0][b + 3]);
+        const double mz = zk[0][b] - sqrt(zk[0][b + 1] * zk[0][b + 1] + zk[0][b + 2] * zk[0][b + 2] + zk[0][b + 3] * zk[0][b + 3]);
+        const double d = push(fmax(ms, 0.0), fmax(mz, 0.0));
+        sk[0][b] += d - fmin(ms, 0.0);
+        zk[0][b] += d - fmin(mz, 0.0);
+      }
+      double u[6], dv[3], dw[3];
+      compute_u(u);
+      lin(u, dv, dw);
+#pragma unroll
+      for (int l = 0; l < NR; ++l) {
+        const double sl = fmax(rowval(l, dv, dw), 0.0), zl = fmax(wrec[28 + DAT_MAXROW + l], 0.0);
+        const double d = act(l) * push(sl, zl);
+        rst.set_sz(l, act(l) > 0.0 ? sl + d : fmax(rowval(l, dv, dw), S0), act(l) * (zl + d));
+      }
+    }
+  }
 
   // scales for the relative stopping rule
   {
@@ -985,6 +1146,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
   BK() = 1e300;
   out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
   const double ideg = 1.0 / (double)(3 * grp.nblk(NB) + __builtin_popcount(mask));
+  int bk_it = 0;  // WS: the iteration of the last halving of the best in-band merit (stall exit)
 
   DAT_PHASE_INIT(0);
   for (int it = 0;; ++it) {
@@ -1112,6 +1274,24 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
         out.merit = merit;
 #pragma unroll
         for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
+        if constexpr (WS) {
+          if (wrec) {  // the converged iterate: the next pass's warm start
+#pragma unroll
+            for (int c = 0; c < 3; ++c) wrec[1 + c] = y[0][c];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) wrec[4 + r] = w[r];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) { wrec[10 + j] = sk[0][j]; wrec[19 + j] = zk[0][j]; }
+#pragma unroll
+            for (int l = 0; l < NR; ++l) {
+              double sl, zl;
+              rst.sz(l, sl, zl);
+              wrec[28 + l] = sl;
+              wrec[28 + DAT_MAXROW + l] = zl;
+            }
+            wrec[0] = 1.0;
+          }
+        }
         DAT_PHASE(8);
         return out;
       }
@@ -1124,6 +1304,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
       // Clarabel's own tolerance.
       const double mclr = fmax(fmax(pres / nh, dres / nq), gap * frcp(fmax(1.0, fabs(pobj))));
       const bool band = fmax(pres / nh, dres / nq) < 1e-7 && mclr < 1e-6;
+      const bool prog = band && mclr < 0.5 * BK();  // (WS: the stall exit below)
       if (band && mclr < BK()) {
         BK() = mclr;
 #pragma unroll
@@ -1135,6 +1316,32 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
           best[3 * NB + r] = w[r];
           best[3 * NB + 6 + r] = pi[r];
           best[3 * NB + 12 + r] = u[r];
+        }
+      }
+      if (WS && wson) {
+        // stall exit (the tail kernel): an in-band iterate WS_STALL_TOL (ten times inside Clarabel's tolerance)
+        // is recorded and the merit has not halved in WS_STALL_ITS iterations -- the Newton systems of a stalled
+        // ADMM loop's agent QP resolve no further; its best in-band iterate is returned (OPTIMAL, in band)
+        if (prog) bk_it = it;
+        if (BK() <= WS_STALL_TOL && it - bk_it >= WS_STALL_ITS) {
+          out.why = 7;
+          if (wrec) {  // the current iterate (in band): the next pass's warm start
+#pragma unroll
+            for (int c = 0; c < 3; ++c) wrec[1 + c] = y[0][c];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) wrec[4 + r] = w[r];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) { wrec[10 + j] = sk[0][j]; wrec[19 + j] = zk[0][j]; }
+#pragma unroll
+            for (int l = 0; l < NR; ++l) {
+              double sl, zl;
+              rst.sz(l, sl, zl);
+              wrec[28 + l] = sl;
+              wrec[28 + DAT_MAXROW + l] = zl;
+            }
+            wrec[0] = 1.0;
+          }
+          break;
         }
       }
       BM() = fmin(BM(), merit);
@@ -1935,25 +2142,28 @@ DAT_HD bool ipm_unclean(const IPMOut& r) {
   return r.status == ST_INACCURATE || (r.status == ST_OPTIMAL && r.inband && r.merit > IPM_CLARABEL_TOL);
 }
 template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = RowRegs, unsigned AUXM = 0,
-          class GRP = NoGrp, int ROBUST = IPM_FAST>
+          class GRP = NoGrp, int ROBUST = IPM_FAST, bool WS = false>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
-                        GRP grp = GRP{}) {
+                        GRP grp = GRP{}, double* wrec = nullptr, bool wson = false) {
   if constexpr (ROBUST == IPM_FAST_REDO) {
     // trip 0 fast; trip 1 robust (the fast outcome not clean); trip 2 fast once more when the robust outcome
     // is worse (deterministic: it reproduces the first; keeping the first iterate instead would hold another
     // y, w, pi, u live across the robust solve).  One call site per instantiation (ipm_attempt is inlined
     // into each: an instance called from two sites is compiled out of line, which cost k_cadmm 7 %).
+    // WS: trip 0 may start warm (the record's flag); trip 2 restores the flag so that it reproduces trip 0.
     IPMOut o, f;
     int done = 0, done_refs = 0, done_corrs = 0;
+    const double wflag = (WS && wrec) ? wrec[0] : 0.0;
 #pragma unroll 1
     for (int trip = 0;; ++trip) {
-      if (trip == 1)
-        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                           tol, rw, grp);
+      if (WS && wrec && trip == 2) wrec[0] = wflag;
+      if (trip == 1 || (wson && wflag == 1.0))  // a warm first trip (and its rerun, trip 2) runs the robust solver
+        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST, WS>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                               tol, rw, grp, wrec, wson);
       else
-        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_R>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                           tol, rw, grp);
+        o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_R, WS>(sh, er, rt, P, y0, y, w, best, max_iter,
+                                                                               tol, rw, grp, wrec, wson);
       o.iters += done;
       o.refs += done_refs;
       o.corrs += done_corrs;
@@ -1989,15 +2199,30 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
     int rank0 = 0;  // first attempt: 0 converged, 1 in-band OPTIMAL, 2 not OPTIMAL
     double merit0 = 0.0;
     IPMOut o;
+    if constexpr (WS) {
+      if (wson && wrec && wrec[0] == 1.0) start = 3;  // the warm attempt first (a converged previous pass)
+    }
 #pragma unroll 1
     for (;;) {
-      // (the tuned start as the first attempt is capped at 20 iterations: see above)
-      o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, ROB>(
-          sh, er, rt, P, y0, y, w, best, start == 1 && trip != 1 && max_iter > 20 ? 20 : max_iter, tol, rw, grp,
-          start);
+      // (the tuned start as the first attempt is capped at 20 iterations: see above; the warm one at WS_MAXIT)
+      o = ipm_attempt<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, ROB, WS>(
+          sh, er, rt, P, y0, y, w, best,
+          start == 3 ? (max_iter > WS_MAXIT ? WS_MAXIT : max_iter)
+                     : start == 1 && trip != 1 && max_iter > 20 ? 20 : max_iter,
+          tol, rw, grp, start, wrec, wson);
       o.iters += done;
       o.refs += done_refs;
       o.corrs += done_corrs;
+      if (WS && start == 3) {
+        // the warm attempt: converged cleanly, stalled in band within WS_STALL_TOL (or certified), else the cold
+        // sequence from its first start
+        if ((o.why == 0 && !o.inband) || o.why == 7 || o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
+        start = first;
+        done = o.iters;
+        done_refs = o.refs;
+        done_corrs = o.corrs;
+        continue;
+      }
       if (trip == 2) break;
       if (trip == 1) {
         const int r1 = ipm_rank(o);
@@ -2006,7 +2231,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       } else {
         if (o.status == ST_FAILED || o.status == ST_INFEASIBLE) break;
         if (start == 1) {
-          if (o.why == 0 && !o.inband) break;
+          if ((o.why == 0 && !o.inband) || (WS && o.why == 7)) break;
           start = 0;
         } else {
           if (!(o.status == ST_OPTIMAL && o.inband && o.merit > IPM_CLARABEL_TOL)) break;
@@ -2020,20 +2245,25 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       done_refs = o.refs;
       done_corrs = o.corrs;
     }
+    if constexpr (WS) {  // only a converged solve leaves a warm start for the next pass
+      if (wrec && !(o.status == ST_OPTIMAL && ((o.why == 0 && !o.inband) || o.why == 7))) wrec[0] = 0.0;
+    }
     return o;
   }
 }
 
 // Solve with the smallest row-slot instantiation that covers every lane of the wavefront
 // (nr_wave: wave-uniform maximum of rows_needed over the lanes taking part).
-template <int MODE, int NB, int ROBUST = IPM_FAST, class SH, class ER, class RT>
+template <int MODE, int NB, int ROBUST = IPM_FAST, bool WS = false, class SH, class ER, class RT>
 DAT_HD IPMOut ipm_solve_rows(int nr_wave, const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
-                             const double* y0, double y[NB][3], double w[6], double* best, int max_iter, double tol) {
+                             const double* y0, double y[NB][3], double w[6], double* best, int max_iter, double tol,
+                             double* wrec = nullptr, bool wson = false) {
   if (nr_wave <= NBASE)
-    return ipm_solve<MODE, NB, NBASE, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                             tol);
-  return ipm_solve<MODE, NB, DAT_MAXROW, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST>(sh, er, rt, P, y0, y, w, best,
-                                                                                max_iter, tol);
+    return ipm_solve<MODE, NB, NBASE, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST, WS>(sh, er, rt, P, y0, y, w, best,
+                                                                                 max_iter, tol, RowRegs{}, NoGrp{}, wrec, wson);
+  return ipm_solve<MODE, NB, DAT_MAXROW, SH, ER, RT, RowRegs, 0, NoGrp, ROBUST, WS>(sh, er, rt, P, y0, y, w, best,
+                                                                                    max_iter, tol, RowRegs{}, NoGrp{},
+                                                                                    wrec, wson);
 }
 
 }  // namespace dat

@@ -191,13 +191,26 @@ int dat_get_inband_exits(dat_handle* h, long long* inband, long long* beyond_cla
 /* IPM iterative-refinement passes run and corrections applied by every kernel since the last counter
  * reset: the executed-work terms of the flop model. */
 int dat_get_refinement_counters(dat_handle* h, long long* passes, long long* corrections);
-/* C-ADMM control steps of a scenario finished by the robust kernel since the last counter reset: k_cadmm
- * hands a scenario's step to k_cadmm_rob, at the ADMM pass it is in, when one of its agent QPs does not
+/* C-ADMM control steps of a scenario finished by the tail kernel since the last counter reset: k_cadmm
+ * hands a scenario's step to k_cadmm_tail, at the ADMM pass it is in, when one of its agent QPs does not
  * end cleanly (INACCURATE, or accepted in band beyond Clarabel's 1e-8: inside the reference's max_iter
- * stalls next to trees), and k_cadmm_rob redoes those QPs with the robust solver (stiff rows in augmented
- * form) and finishes the step.  Replaces no reference call (Clarabel's internal KKT regularisation); the
- * per-QP surfaces (dat_solve_agent_qp_batch) redo the QP themselves. */
+ * stalls next to trees) or, with a forest, when the tail rule holds for its next pass (the previous step took
+ * more than 20 ADMM passes, or the pass is the 16th); k_env_class routes a scenario whose previous step took
+ * more than 20 passes to the tail before the step.  k_cadmm_tail redoes unclean QPs with the robust solver
+ * (stiff rows in augmented form) and finishes the step.  Replaces no reference call (Clarabel's internal KKT
+ * regularisation); the per-QP surfaces (dat_solve_agent_qp_batch) redo the QP themselves. */
 int dat_get_robust_redos(dat_handle* h, long long* redos);
+/* The tail kernel's work since the last counter reset (out[6]): [0] ADMM passes, [1] the sum over its passes of
+ * the slowest agent QP's IPM iterations (the critical path of the stalled steps), [2] scenario-steps routed to
+ * the tail before the step, [3] agent QPs whose rows were certified infeasible (a Farkas certificate on the dvl
+ * rows: the QP is held at its previous solution, as the reference holds it when Clarabel reports infeasible,
+ * control/rqp_cadmm.py:496-499), [4] solves ended by the stall exit, [5] warm-started solves.  Replaces no
+ * reference call. */
+int dat_get_tail_counters(dat_handle* h, long long* out);
+/* C-ADMM with a forest: scenario-steps with a collision flag and the smallest minimum env distance over every
+ * HL step since the last counter reset (the reference logs min_env_dist per step and flags a collision below
+ * its threshold: example/rqp_example.py:129, example/env_forest.py:158-159; +inf without a forest). */
+int dat_get_collision_stats(dat_handle* h, long long* collisions, double* min_env_dist);
 /* Device time [ms] of the last dat_solve_agent_qp_batch launch (k_agent_qp; HIP events on the handle's
  * stream): the solve_time RQPPrimalSolver.solve returns (Clarabel's solver_stats.solve_time,
  * control/rqp_cadmm.py:500, control/rqp_dd.py:497). */

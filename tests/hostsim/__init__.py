@@ -56,6 +56,39 @@ def qp_cadmm_ex(prm, n, st, acc, lhs, rhs, i, lam, fbar, rho=1.0, tuned=0):
     return f, status, it.value, ib.value
 
 
+def _qp_consts():
+    """WREC_SIZE and the tail rule (TAIL_PREV, TAIL_PASS) as dat_qp.hpp defines them"""
+    import re
+
+    src = open(os.path.join(CORE, "dat_qp.hpp")).read()
+    tp = re.search(r"constexpr int TAIL_PREV = (\d+), TAIL_PASS = (\d+);", src)
+    assert tp and "constexpr int WREC_SIZE = 28 + 2 * DAT_MAXROW;" in src
+    return 28 + 2 * 13, int(tp.group(1)), int(tp.group(2))
+
+
+WREC_SIZE, TAIL_PREV, TAIL_PASS = _qp_consts()
+
+
+def qp_cadmm_warm(prm, n, st, acc, lhs, rhs, i, lam, fbar, rho, wrec, wson=True, tuned=0):
+    """hs_qp_cadmm_ex as the tail kernel solves it: the certificate of infeasible rows, the warm-start record wrec
+    (WREC_SIZE doubles, updated in place) and, wson, the warm first attempt (wrec[0] = 1) and the stall exit;
+    returns (f, status, iters, inband)"""
+    f = np.zeros(3 * n)
+    it, ib = ctypes.c_int(), ctypes.c_int()
+    lhs = np.ascontiguousarray(lhs, dtype=np.float64).reshape(-1, 3)
+    assert wrec.dtype == np.float64 and wrec.flags.c_contiguous and wrec.size == WREC_SIZE
+    status = lib().hs_qp_cadmm_warm(p(prm), n, p(st), p(acc), p(lhs), p(rhs), lhs.shape[0], i, p(lam), p(fbar),
+                                    ctypes.c_double(rho), int(tuned), wrec.ctypes.data_as(D), int(bool(wson)), f.ctypes.data_as(D),
+                                    ctypes.byref(it), ctypes.byref(ib))
+    return f, status, it.value, ib.value
+
+
+def last_stiff():
+    """the last C-ADMM hostsim solve was redone robustly (its fast attempt was not clean: the GPU hands the
+    scenario to the tail there)"""
+    return lib().hs_last_stiff()
+
+
 def last_diag():
     """(merit, inband, exit reason) of the last hostsim QP solve"""
     m, ib, why = ctypes.c_double(), ctypes.c_int(), ctypes.c_int()

@@ -75,6 +75,9 @@ int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc
 // stiff exits of the fast solver since the last call (hs_qp_cadmm_ex: the redo count of IPM_FAST_REDO)
 long long g_stiff_redo = 0;
 long long hs_stiff_redos() { return g_stiff_redo; }
+int g_last_stiff = 0;
+// the last solve was redone robustly (IPM_FAST_REDO: its fast attempt was not clean)
+int hs_last_stiff() { return g_last_stiff; }
 int hs_qp_cadmm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
                 const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
                 double* f_out, int* iters) {
@@ -100,12 +103,58 @@ int hs_qp_cadmm_ex(const double* prm, int n, const double* st, const double* acc
   set_env_rows(P, E, S, mask, lhs, rhs);
   lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
   P.tuned = tuned;
+  // the GPU's C-ADMM agent QP (k_cadmm / k_cadmm_tail): rows certified infeasible are held; the fast solver,
+  // redone robustly when not clean
+  if (dvl_rows_infeasible(PlainRef<QPShared>{&S}, EnvPlain{&E}, P.emask)) P.infeasible = 1;
   double y[1][3], w[6], best[best_size(1)];
-  // the GPU's C-ADMM agent QP (k_cadmm / k_cadmm_rob): the fast solver, redone robustly when not clean
   IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO>(rows_needed(P.emask), PlainRef<QPShared>{&S}, EnvPlain{&E},
                                                           RtPtr{Rt_all + 9 * i}, P, prm + DAT_P_FEQ(n) + 3 * i, y, w,
                                                           best, 50, HS_TOL);
   if (o.stiff) ++g_stiff_redo;
+  g_last_stiff = o.stiff;
+  *inband = o.inband ? 10 * o.why + 1 : 0;
+  diag(o);
+  for (int j = 0; j < n; ++j) {
+    if (j == i) {
+      for (int c = 0; c < 3; ++c) f_out[3 * j + c] = y[0][c];
+    } else {
+      cadmm_free_block(Rt_all + 9 * j, lam + 3 * j, fbar + 3 * j, o.pi, rho, f_out + 3 * j);
+    }
+  }
+  *iters = o.iters;
+  return o.status;
+}
+
+// as hs_qp_cadmm_ex with the tail kernel's agent QP: the certificate of infeasible rows, the warm-start record
+// (wrec: WREC_SIZE doubles, in / out: the converged iterate is recorded) and, wson != 0, the warm first attempt
+// (when wrec[0] = 1) and the stall exit
+int hs_qp_cadmm_warm(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
+                     const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
+                     int tuned, double* wrec, int wson, double* f_out, int* iters, int* inband) {
+  if (nenv > DAT_NENV) return -1;
+  double Rt_all[16 * 9];
+  const double* Rl = st + DAT_S_RL(n);
+  for (int j = 0; j < n; ++j) make_Rt(prm + DAT_P_RCOM(n) + 3 * j, Rl, Rt_all + 9 * j);
+  QPShared S;
+  build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+  QPLane<1> P;
+  lane_cadmm_static(P, prm, i);
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  unsigned mask;
+  env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
+  EnvRows E;
+  set_env_rows(P, E, S, mask, lhs, rhs);
+  lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
+  P.tuned = tuned;
+  // the tail kernel's certificate of infeasible rows (k_cadmm_tail, at the scenario's hand-over)
+  if (dvl_rows_infeasible(PlainRef<QPShared>{&S}, EnvPlain{&E}, P.emask)) P.infeasible = 1;
+  double y[1][3], w[6], best[best_size(1)];
+  IPMOut o = ipm_solve_rows<MODE_CADMM, 1, IPM_FAST_REDO, true>(rows_needed(P.emask), PlainRef<QPShared>{&S},
+                                                                EnvPlain{&E}, RtPtr{Rt_all + 9 * i}, P,
+                                                                prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50, HS_TOL, wrec,
+                                                                wson != 0);
+  if (o.stiff) ++g_stiff_redo;
+  g_last_stiff = o.stiff;
   *inband = o.inband ? 10 * o.why + 1 : 0;
   diag(o);
   for (int j = 0; j < n; ++j) {

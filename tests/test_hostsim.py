@@ -9,6 +9,7 @@ from oracle import model as om
 from oracle import scenarios as osc
 from oracle.ipm import OPTIMAL, solve_qp
 from tests import hostsim as hs
+from tests.hostsim import TAIL_PASS, TAIL_PREV
 from tests._golden import load, state_from
 
 
@@ -181,10 +182,10 @@ def test_c4_stall_stretch_matches_oracle():
     """The C4 stall stretches of ref_c4_hard.npz (tests/golden/make_c4_hard.py, n = 6 in seeded forests,
     101-pass ADMM stalls from the second step on) with every agent QP answered by the host build of the
     device solver as the GPU's C-ADMM step runs it (IPM_FAST_REDO: the fast solver, redone robustly when
-    not clean): ADMM iteration counts exact and f_des within max(1e-5, 5 x the oracle's own sensitivity)
-    at every step (or the reference's own spread at Clarabel's 1e-8, f_des_1e8).  The first 12 steps of
-    both stretches (the round-4 solver left the oracle by 2e-4 at steps 16-17 of the second; the GPU test
-    runs all 20)."""
+    not clean; rows certified infeasible held; the tail rule's warm start and stall exit from the second
+    pass of every wedged step): ADMM iteration counts exact and f_des within max(1e-5, 5 x the oracle's own
+    sensitivity) at every step (or the reference's own spread at Clarabel's 1e-8, f_des_1e8), no accept
+    beyond Clarabel's 1e-8.  The first 12 steps of both stretches (the GPU test runs all 20)."""
     from distributed_aerial_transportation_amd import scenarios
     from distributed_aerial_transportation_amd.system import RQPState, pack_state
     from oracle import controllers as oc
@@ -200,25 +201,38 @@ def test_c4_stall_stretch_matches_oracle():
         s0 = RQPState.unpack(d["x0"][j], n)
         st = om.State(s0.R, s0.w, s0.xl, s0.vl, s0.Rl, s0.wl, project=False)
         ctl = oc.CADMM(p, osc.col_radius(n), forest)
-        tally = {"pass": 0, "tuned": 1, "loose": 0}
+        tally = {"pass": 0, "tuned": 1, "loose": 0, "prev": 0, "tail": False, "unclean": False}
+        wrec = np.zeros((n, hs.WREC_SIZE))
 
         def solve(self, i, s_, acc, env, rho):
             lam = self.lam[:, :, i].T.reshape(-1).copy()
             fbar = self.f_mean.T.reshape(-1).copy()
-            tuned = tally["tuned"] if tally["pass"] == 0 else 0
-            f, status, _, inb = hs.qp_cadmm_ex(prm, n, pack_state(s_), np.concatenate(acc), env.lhs, env.rhs, i, lam,
-                                               fbar, rho, tuned=tuned)
+            ps = tally["pass"]
+            tuned = tally["tuned"] if ps == 0 else 0
+            # the tail rule (dat_qp.hpp TAIL_PREV / TAIL_PASS): warm start + stall exit in the passes it names;
+            # the passes the tail kernel runs keep the warm-start records
+            wson = ps >= 1 and (tally["prev"] > TAIL_PREV or ps >= TAIL_PASS)
+            tally["tail"] = tally["tail"] or ps >= TAIL_PASS
+            rec = np.ascontiguousarray(wrec[i]) if tally["tail"] else np.zeros(hs.WREC_SIZE)
+            f, status, _, inb = hs.qp_cadmm_warm(prm, n, pack_state(s_), np.concatenate(acc), env.lhs, env.rhs, i, lam,
+                                                 fbar, rho, rec, wson=wson, tuned=tuned)
+            if tally["tail"]:
+                wrec[i] = rec
             tally["loose"] += bool(inb) and hs.last_diag()[0] > 1e-8
+            tally["unclean"] = tally["unclean"] or bool(hs.last_stiff())
             if status == 0:
                 self.prev_f[i] = f.reshape(n, 3).T.copy()
             if i == n - 1:
                 tally["pass"] += 1
+                tally["tail"] = tally["tail"] or tally["unclean"]
             return self.prev_f[i], None
 
         ctl.solve_agent = solve.__get__(ctl)
         prev = 0
         for k in range(K):
-            tally["pass"], tally["tuned"] = 0, 1 if prev <= 3 else 0
+            tally["pass"], tally["tuned"], tally["prev"] = 0, 1 if prev <= 3 else 0, prev
+            tally["tail"], tally["unclean"] = prev > TAIL_PREV, False
+            wrec[:] = 0.0
             acc, _, _ = oc.desired_acceleration_forest(st, forest)
             f, stat = ctl.control(st, acc)
             prev = stat.iter
