@@ -422,26 +422,37 @@ def sustained_loop(eng, states, steps: int, block: int, barrier, dist, dev, n: i
         dt = time.perf_counter() - t0
         barrier()
         w = eng.work()
+        # (the minimum env distance enters as its negative, so that one "max" reduction carries both maxima)
         rows.append([dt, w["qp_solves"], w["ipm_iters"], w.get("inband_exits", 0),
-                     w.get("inband_beyond_clarabel_tol", 0), w.get("robust_redos", 0), k])
+                     w.get("inband_beyond_clarabel_tol", 0), w.get("robust_redos", 0), k, w.get("collisions", 0),
+                     -w.get("min_env_dist", np.inf), w.get("tail_routed", 0), w.get("certified_infeasible", 0),
+                     w.get("stall_exits", 0), w.get("tail_passes", 0), w.get("tail_critical_ipm_iters", 0)])
     rows = np.array(rows, dtype=np.float64)
     if dist is not None:
         from distributed_aerial_transportation_amd.sharding import reduce_values
 
         mx = reduce_values(rows.reshape(-1), "max", dev).reshape(rows.shape)
         rows = reduce_values(rows.reshape(-1), "sum", dev).reshape(rows.shape)
-        rows[:, 0], rows[:, 6] = mx[:, 0], mx[:, 6]
+        rows[:, 0], rows[:, 6], rows[:, 8] = mx[:, 0], mx[:, 6], mx[:, 8]
     blocks = []
     b0 = 0
-    for dt, q, ip, ib, lo, rr, k in rows:
+    for dt, q, ip, ib, lo, rr, k, col, nmd, trt, cert, stx, tps, tcr in rows:
         blocks.append({"hl_steps": f"{b0}-{b0 + int(k) - 1}", "ms_per_step": dt / k * 1e3, "qp_per_s": q / dt,
                        "mean_admm_passes": q / (batch_all * n * k), "ipm_iters_per_qp": ip / max(q, 1),
-                       "inband_exits": int(ib), "inband_beyond_clarabel_tol": int(lo), "robust_redos": int(rr)})
+                       "inband_exits": int(ib), "inband_beyond_clarabel_tol": int(lo), "robust_redos": int(rr),
+                       # scenario-steps with the reference's collision flag (example/env_forest.py:158-159) and the
+                       # smallest min env distance of the block (example/rqp_example.py:129)
+                       "collisions": int(col), "min_env_dist": float(-nmd),
+                       # the tail (k_cadmm_tail): scenario-steps routed before the step, agent QPs certified
+                       # infeasible, stall exits, its passes and their critical-path IPM iterations
+                       "tail_routed": int(trt), "certified_infeasible": int(cert), "stall_exits": int(stx),
+                       "tail_passes": int(tps), "tail_critical_ipm_per_pass": tcr / max(tps, 1)})
         b0 += int(k)
     T, Q = rows[:, 0].sum(), rows[:, 1].sum()
     return {"hl_steps": steps, "block": block, "ms_per_step": T / steps * 1e3, "qp_per_s": Q / T,
             "slowest_block_ms_per_step": max(b["ms_per_step"] for b in blocks),
             "inband_beyond_clarabel_tol": int(rows[:, 4].sum()), "robust_redos": int(rows[:, 5].sum()),
+            "collisions": int(rows[:, 7].sum()), "min_env_dist": float(-rows[:, 8].max()),
             "blocks": blocks}
 
 

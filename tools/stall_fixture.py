@@ -37,7 +37,10 @@ for j in range(J):
                "ipm_iters": w["ipm_iters"], "qp_solves": w["qp_solves"],
                "ipm_per_qp": w["ipm_iters"] / max(w["qp_solves"], 1), "inband": w["inband_exits"],
                "loose": w["inband_beyond_clarabel_tol"], "handovers": w["robust_redos"], "f_des_rel": rel,
-               "iters_ref": int(d["iters"][j, k])}
+               "iters_ref": int(d["iters"][j, k]), "tail_passes": w.get("tail_passes"),
+               "tail_crit_ipm": w.get("tail_critical_ipm_iters"), "routed": w.get("tail_routed"),
+               "certified": w.get("certified_infeasible"), "stall_exits": w.get("stall_exits"),
+               "warm": w.get("warm_starts")}
         if k > 0:
             tot_ms += ms
             tot_pass += p
