@@ -440,18 +440,23 @@ class _PrimalSolver:
 class RQPCADMMPrimalSolver(_PrimalSolver):
     """control/rqp_cadmm.py:26-507: solve(state, acc_des, lambda_f, cadmm_rho, f_mean) ->
     (f (3, n), solve_time, collision, min_env_dist).  Exception -> f_eq (:491-494); non-OPTIMAL ->
-    previous solution (:496-499).  cadmm_rho defaults to 0 as in the reference (:487), which calls rho = 0 only
-    in its constructor's warm-up solve (:131-140), where the copies f_j, j != i, are not unique (that solve
-    only seeds Clarabel's warm start): rho <= 0 -- the default included -- raises ValueError instead of
-    silently solving another QP."""
+    previous solution (:496-499).  The reference's default cadmm_rho = 0 (:487) is used only by its
+    constructor's warm-up solve (:131-140), where the copies f_j, j != i, are not unique (that solve only seeds
+    Clarabel's warm start); here cadmm_rho defaults to the controller's initial penalty rho0 = 1
+    (control/rqp_cadmm.py:564), and an explicit rho <= 0 raises ValueError instead of silently solving another
+    QP."""
 
     _mode = L.MODE_CADMM
 
     def _set_warm_start(self) -> None:
         self.prev_f = self.f_eq.copy()
 
-    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: float = 0.0, f_mean=None):
+    RHO0 = 1.0  # RQPCADMMController.rho0 (control/rqp_cadmm.py:564)
+
+    def solve(self, state, acc_des, lambda_f=None, cadmm_rho: Optional[float] = None, f_mean=None):
         n = self.n
+        if cadmm_rho is None:
+            cadmm_rho = self.RHO0
         if not float(cadmm_rho) > 0.0:
             raise ValueError(f"cadmm_rho must be > 0 (got {cadmm_rho}): at rho = 0 the agent QP's copies f_j, "
                              "j != i, are not unique (the reference uses rho = 0 only for its constructor's "

@@ -137,11 +137,13 @@ __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NC
   }
   return m;
 }
-// dynamic LDS of a k_cadmm_tail workgroup (one scenario slot, rmode 3)
+// dynamic LDS of a k_cadmm_tail workgroup (one scenario slot, rmode 3), with the n lanes' IPM scratch records
+// (best iterate, stiff-row columns and Schur factor: best_size(1) doubles each) behind the class's area: the
+// robust solver's stiff-row loops read and write them at every iteration, an LDS round trip instead of L2 / HBM
 __host__ __device__ inline size_t cadmm_tail_lds_bytes(int n, int max_cls = NCLS - 1) {
   size_t m = 0;
   for (int c = 0; c <= max_cls; ++c) {
-    const size_t b = cadmm_fixed_bytes(n, 1) + sizeof(double) * cadmm_area_doubles(c, 3);
+    const size_t b = cadmm_fixed_bytes(n, 1) + sizeof(double) * (cadmm_area_doubles(c, 3) + al2((size_t)n * best_size(1)));
     m = b > m ? b : m;
   }
   return m;
@@ -540,12 +542,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     // ---- refill empty slots from the queue
     DAT_PHASE(11);
     if (lane < NT && i == 0 && L.sid[ls] == -1) {
-      int s2;
-      for (;;) {
-        const int q = atomicAdd(qh, 1);
-        s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
-        break;
-      }
+      const int q = atomicAdd(qh, 1);
+      const int s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
       L.sid[ls] = s2;
       L.done[ls] = 0;
       L.wmx[ls] = RB && !TM && s2 >= 0 ? a.rres[(size_t)s2 * RRES_INTS + RRES_WMX] : 0;
@@ -562,7 +560,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
-      bst = a.best + ((size_t)sc * n + i) * (RB ? best_size(1) : best_rec(1));
+      // (the tail: the lane's record in LDS, behind the env image -- a generic pointer, flat loads go to LDS)
+      bst = RB ? L.env + env_lds_doubles(NE) + i * best_size(1) : a.best + ((size_t)sc * n + i) * best_rec(1);
       iter = 0;
       prev_iter = a.iters[sc];  // the previous step's ADMM iterations (rewritten when the scenario stops)
       qstat = ST_OPTIMAL;
@@ -1966,6 +1965,9 @@ KArgs kargs(dat_handle* h) {
   a.tail_prev = h->nforest > 0 ? TAIL_PREV : INT_MAX;
   a.tail_pass = h->nforest > 0 ? TAIL_PASS : INT_MAX;
   a.tmode = 0;
+#ifdef DAT_NO_TAIL  // A/B builds only (tools/build_var.sh): the round-5 schedule, no tail rule
+  a.tail_prev = a.tail_pass = INT_MAX;
+#endif
   return a;
 }
 
@@ -2238,6 +2240,14 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     std::string m = g_err;
     dat_destroy(h);
     return fail(m);
+  }
+  if (c.mode == DAT_MODE_CADMM) {  // the tail's workgroup may exceed the default 64 KB of dynamic LDS
+    const int tl = (int)cadmm_tail_lds_bytes(c.n);
+    if (hipFuncSetAttribute((const void*)k_cadmm_tail, hipFuncAttributeMaxDynamicSharedMemorySize, tl) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_cadmm0_tail, hipFuncAttributeMaxDynamicSharedMemorySize, tl) != hipSuccess) {
+      dat_destroy(h);
+      return fail("dat_create: tail kernel LDS attribute");
+    }
   }
   // LDS budgets
   size_t lds = c.mode == DAT_MODE_CADMM ? cadmm_lds_bytes(c.n, 64 / c.n) : (c.mode == DAT_MODE_DD ? dd_setup_lds(c.n) : 0);

@@ -37,6 +37,11 @@ constexpr int NBASE = 3;          // base slots shared by all agents of a scenar
 // six to keep the dual residual below the stopping tolerance (tools/hard_qp_probe.py: 2 passes left
 // 281 of 798 such solves at in-band exits, 6 passes 69, all within 1.5e-6 of the oracle)
 constexpr int NREF = 6;
+// The robust instantiation (stiff rows in augmented form) at most two: on the C4 stall stretches (host build,
+// tools/stall_warm_hostsim.py) its warm-started solves ran 4.75 refinement passes and 4.43 corrections per IPM
+// iteration with six -- most stop at the cap, the residual of the augmented system does not reach the rounding
+// test -- and 1.9 / 1.7 with two, at the same IPM iterations per solve (8.5) and f_des within 1.4e-6 of the oracle
+constexpr int NREF_ROB = 2;
 // Initial point: cone / row slacks shifted to at least IPM_S0 inside, duals IPM_Z0 e.  The agent QPs'
 // multipliers are O(1e-2) at the solution; starting the duals and the slack margins there instead of at 1
 // takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU sweep over
@@ -189,12 +194,17 @@ DAT_HD constexpr int best_size(int NB) {
 // Clarabel's own tolerance: an in-band exit whose merit is above it is one Clarabel would not certify
 constexpr double IPM_CLARABEL_TOL = 1e-8;
 
-// Warm start (start 3, ipm_solve WS): the previous ADMM pass's converged iterate of the same agent QP, in a
-// lane record of WREC_SIZE doubles -- [0] valid flag, y (3), w (6), cone slacks (9) and duals (9), the row
-// slacks and duals (DAT_MAXROW each) -- pushed back into the interior so that every complementarity pair's
-// product is at least WS_MU (a pair (s, z) below it moves to (s + d, z + d); a second-order cone pair by its
-// margins s0 - |s1:3|, z0 - |z1:3|).  The attempt is capped at WS_MAXIT iterations; one that does not converge
-// cleanly goes on to the cold starts.
+// Warm start (start 3, ipm_solve WS): the previous ADMM pass's last iterate of the same agent QP (of a converged,
+// stall-exited or in-band OPTIMAL solve), in a lane record of WREC_SIZE doubles -- [0] valid flag, y (3), w (6),
+// cone slacks (9) and duals (9), the row slacks and duals (DAT_MAXROW each) -- pushed back into the interior so
+// that every complementarity pair's product is at least WS_MU (a pair (s, z) below it moves to (s + d, z + d); a
+// second-order cone pair by its margins s0 - |s1:3|, z0 - |z1:3|), and solved by the robust instantiation (the
+// stall's active rows carry barrier weights of 1e10 and more from the first iteration).  The attempt is capped at
+// WS_MAXIT iterations; one that does not end cleanly goes on to the cold starts.  Host build, C4 stall stretches
+// (2 x 20 HL steps of 101-pass stalls, tools/stall_warm_hostsim.py): the critical path (the slowest agent QP of
+// every pass) 25-32 IPM iterations per pass cold, ~10 warm; f_des within 2.2e-6 of the oracle where it is
+// reproducible.  WS_MU in 1e-2 .. 1e3 measured alike (42-49 k critical iterations over the stretches); 1e2 has
+// the smallest f_des difference.
 constexpr double WS_MU = 1e2;
 constexpr int WS_MAXIT = 30;
 // stall exit of the tail kernel's solves (ipm_attempt WS): best in-band merit <= WS_STALL_TOL and not halved
@@ -573,8 +583,6 @@ DAT_HD bool soc_scaling(const double* s, const double* z, SocScale& S) {
   S.eta = sqrt(sn * izn);
   S.ieta = frcp(S.eta);
   S.k1 = frcp(1.0 + S.w0);
-  S.w0 = S.w0; S.w1 = S.w1; S.w2 = S.w2; S.w3 = S.w3;
-  S.eta = S.eta; S.ieta = S.ieta; S.k1 = S.k1;
   return true;
 }
 // o = W v (inv = false) or W^-1 v (inv = true); W = eta H(w), W^-1 = H(Jw)/eta
@@ -1147,6 +1155,27 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
   out.status = ST_INACCURATE;  // until converged (or failed on non-finite data)
   const double ideg = 1.0 / (double)(3 * grp.nblk(NB) + __builtin_popcount(mask));
   int bk_it = 0;  // WS: the iteration of the last halving of the best in-band merit (stall exit)
+  // WS: the current iterate into the warm-start record (the next ADMM pass's start)
+  auto record = [&]() {
+    if constexpr (WS) {
+      if (wrec) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) wrec[1 + c] = y[0][c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) wrec[4 + r] = w[r];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) { wrec[10 + j] = sk[0][j]; wrec[19 + j] = zk[0][j]; }
+#pragma unroll
+        for (int l = 0; l < NR; ++l) {
+          double sl, zl;
+          rst.sz(l, sl, zl);
+          wrec[28 + l] = sl;
+          wrec[28 + DAT_MAXROW + l] = zl;
+        }
+        wrec[0] = 1.0;
+      }
+    }
+  };
 
   DAT_PHASE_INIT(0);
   for (int it = 0;; ++it) {
@@ -1274,24 +1303,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
         out.merit = merit;
 #pragma unroll
         for (int r = 0; r < 6; ++r) { out.pi[r] = pi[r]; out.u[r] = u[r]; }
-        if constexpr (WS) {
-          if (wrec) {  // the converged iterate: the next pass's warm start
-#pragma unroll
-            for (int c = 0; c < 3; ++c) wrec[1 + c] = y[0][c];
-#pragma unroll
-            for (int r = 0; r < 6; ++r) wrec[4 + r] = w[r];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) { wrec[10 + j] = sk[0][j]; wrec[19 + j] = zk[0][j]; }
-#pragma unroll
-            for (int l = 0; l < NR; ++l) {
-              double sl, zl;
-              rst.sz(l, sl, zl);
-              wrec[28 + l] = sl;
-              wrec[28 + DAT_MAXROW + l] = zl;
-            }
-            wrec[0] = 1.0;
-          }
-        }
+        record();  // the converged iterate: the next pass's warm start
         DAT_PHASE(8);
         return out;
       }
@@ -1325,22 +1337,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
         if (prog) bk_it = it;
         if (BK() <= WS_STALL_TOL && it - bk_it >= WS_STALL_ITS) {
           out.why = 7;
-          if (wrec) {  // the current iterate (in band): the next pass's warm start
-#pragma unroll
-            for (int c = 0; c < 3; ++c) wrec[1 + c] = y[0][c];
-#pragma unroll
-            for (int r = 0; r < 6; ++r) wrec[4 + r] = w[r];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) { wrec[10 + j] = sk[0][j]; wrec[19 + j] = zk[0][j]; }
-#pragma unroll
-            for (int l = 0; l < NR; ++l) {
-              double sl, zl;
-              rst.sz(l, sl, zl);
-              wrec[28 + l] = sl;
-              wrec[28 + DAT_MAXROW + l] = zl;
-            }
-            wrec[0] = 1.0;
-          }
+          record();  // the current iterate (in band): the next pass's warm start
           break;
         }
       }
@@ -1369,8 +1366,6 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
       soc_apply(S2[k], zk[k] + 5, l2, false);
 #pragma unroll
       for (int j = 0; j < 4; ++j) { LAM(k, 1 + j) = l1[j]; LAM(k, 5 + j) = l2[j]; }
-      ID0(k) = ID0(k);
-      LAM(k, 0) = LAM(k, 0);
     }
 #ifdef DAT_IPM_TRACE
     for (int k = 0; k < NB; ++k)
@@ -1818,7 +1813,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
       // (a gate skipping the pass when every row's barrier weight z/s < 1 -- tools/ipm_stats.py: no
       // correction was ever applied below z/s = 10 on the C4 loop -- measured slower: C4 k_cadmm 3.74 ->
       // 4.00 ms, the extra live value costs more than the skipped residual)
-      const int nref = corr ? NREF : 0;
+      const int nref = corr ? (ROB ? NREF_ROB : NREF) : 0;
       if (corr) DAT_STAT(0);
 #pragma unroll 1
       for (int ref = 0; ref < nref; ++ref) {
@@ -1904,6 +1899,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
             if (ref == 0) DAT_STAT_H(0);
             break;
           }
+
           if (ref == 0) DAT_STAT_H(1);
         }
         ++out.corrs;
@@ -1928,11 +1924,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
         gs_mul(k, dy[k], g9);
 #pragma unroll
         for (int j = 0; j < 9; ++j) dzs_k[k][j] = tks[j] + g9[j];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) dy[k][c] = dy[k][c];
       }
-#pragma unroll
-      for (int r = 0; r < 6; ++r) { dwv[r] = dwv[r]; du[r] = du[r]; }
     };
     // row directions of the current Newton solution
     // (s_l, z_l) of the row: sl, zl (one pair read by the caller)
@@ -2093,6 +2085,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
   // solve loses accuracy; the minimiser is then still within ~1e-7 of the oracle's), otherwise
   // inaccurate (the reference holds its previous solution).
   if (BK() < 1e300) {
+    record();  // the last iterate of an in-band exit: a start for the next pass all the same
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
@@ -2245,8 +2238,8 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       done_refs = o.refs;
       done_corrs = o.corrs;
     }
-    if constexpr (WS) {  // only a converged solve leaves a warm start for the next pass
-      if (wrec && !(o.status == ST_OPTIMAL && ((o.why == 0 && !o.inband) || o.why == 7))) wrec[0] = 0.0;
+    if constexpr (WS) {  // only an OPTIMAL solve (converged or in band) leaves a warm start for the next pass
+      if (wrec && o.status != ST_OPTIMAL) wrec[0] = 0.0;
     }
     return o;
   }

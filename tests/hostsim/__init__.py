@@ -89,6 +89,13 @@ def last_stiff():
     return lib().hs_last_stiff()
 
 
+def last_work():
+    """(refinement passes, corrections) of the last hostsim QP solve"""
+    r, c = ctypes.c_int(), ctypes.c_int()
+    lib().hs_last_work(ctypes.byref(r), ctypes.byref(c))
+    return r.value, c.value
+
+
 def last_diag():
     """(merit, inband, exit reason) of the last hostsim QP solve"""
     m, ib, why = ctypes.c_double(), ctypes.c_int(), ctypes.c_int()

@@ -30,10 +30,13 @@ void env_slots(const double* env_lhs, const double* env_rhs, int nenv, double lh
 // diagnostics of the last solve (hs_last_diag)
 double g_merit = 0.0;
 int g_inband = 0, g_why = 0;
+int g_refs = 0, g_corrs = 0;
 void diag(const IPMOut& o) {
   g_merit = o.merit;
   g_inband = o.inband;
   g_why = o.why;
+  g_refs = o.refs;
+  g_corrs = o.corrs;
 }
 
 template <int NB>
@@ -63,6 +66,11 @@ int cent_nb_(const double* prm, const double* st, const double* acc, const doubl
 
 extern "C" {
 
+// refinement passes run and corrections applied by the last solve
+void hs_last_work(int* refs, int* corrs) {
+  *refs = g_refs;
+  *corrs = g_corrs;
+}
 void hs_last_diag(double* merit, int* inband, int* why) {
   *merit = g_merit;
   *inband = g_inband;

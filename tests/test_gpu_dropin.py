@@ -121,10 +121,10 @@ def test_gpu_primal_solver_dropins_and_fallbacks():
         f, t, coll, md = ps.solve(s, acc, d[f"cadmm{k}_lam"], 1.0, d[f"cadmm{k}_fm"])
         assert _rel(f, d[f"cadmm{k}_x"][9:].reshape(3, 3, order="F")) < REL
         assert 0.0 < t < 1.0  # the QP kernel's device time [s] (Clarabel's solve_time, control/rqp_cadmm.py:500)
-        # rho defaults to the reference's 0 (control/rqp_cadmm.py:487: its constructor's warm-up solve only,
-        # where the copies f_j are not unique): rejected, explicit or by default
-        with pytest.raises(ValueError):
-            ps.solve(s, acc, d[f"cadmm{k}_lam"], f_mean=d[f"cadmm{k}_fm"])
+        # rho defaults to the controller's rho0 = 1 (the call above, control/rqp_cadmm.py:564); the reference's 0
+        # (:487: its constructor's warm-up solve only, where the copies f_j are not unique) is rejected
+        f1, *_ = ps.solve(s, acc, d[f"cadmm{k}_lam"], f_mean=d[f"cadmm{k}_fm"])
+        assert np.array_equal(f1, f)
         with pytest.raises(ValueError):
             ps.solve(s, acc, d[f"cadmm{k}_lam"], 0.0, d[f"cadmm{k}_fm"])
         # payload upside down: the tilt CBF row 0 . dwl >= cos 15 deg - Rl[2,2] > 0 is infeasible -> hold

@@ -40,7 +40,8 @@ for j in range(J):
                "iters_ref": int(d["iters"][j, k]), "tail_passes": w.get("tail_passes"),
                "tail_crit_ipm": w.get("tail_critical_ipm_iters"), "routed": w.get("tail_routed"),
                "certified": w.get("certified_infeasible"), "stall_exits": w.get("stall_exits"),
-               "warm": w.get("warm_starts")}
+               "warm": w.get("warm_starts"), "refine_passes": w.get("refine_passes"),
+               "refine_corrections": w.get("refine_corrections")}
         if k > 0:
             tot_ms += ms
             tot_pass += p
