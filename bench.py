@@ -13,8 +13,8 @@ rows, up to 101 ADMM iterations of n agent QPs each) + 10 simulation steps (SO(3
     python bench.py --config C2|C3|C5 [--fixed-work]   (QP-level configs of SURVEY.md 8(d))
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-The data path has no collective; torch.distributed (RCCL over xGMI when N > 1) is used for the
-barrier, the max-over-ranks time and an all-gather of the per-scenario metrics.
+The data path has no collective; RCCL over xGMI (sharding.Comm, libdat.so's dat_comm_* C-ABI: no PyTorch in
+the rank processes) carries the barrier, the max-over-ranks time and an all-gather of the per-scenario metrics.
 """
 
 from __future__ import annotations
@@ -311,14 +311,13 @@ def bench_states(n: int, batch: int, rank: int, world: int, forests_n: int, star
     return np.ascontiguousarray(sf), np.ascontiguousarray(st), forests
 
 
-def combine_ranks(dist, world: int, tot: np.ndarray, metrics: np.ndarray, device):
+def combine_ranks(comm, tot: np.ndarray, metrics: np.ndarray):
     """Sum of the work counters, max of the elapsed time, all-gather of the per-scenario metrics (uneven
     shards included) through the package's sharding collectives.  The only collectives of the run (RCCL
-    over xGMI with the nccl backend; gloo on CPU in tests)."""
+    over xGMI: sharding.Comm; the gloo test harness on CPU)."""
     from distributed_aerial_transportation_amd.sharding import gather_rows, reduce_values
 
-    return (reduce_values(tot, "sum", device), reduce_values(tot, "max", device),
-            gather_rows(metrics, device))
+    return reduce_values(tot, "sum", comm), reduce_values(tot, "max", comm), gather_rows(metrics, comm)
 
 
 def spawn_ranks(args) -> int:
@@ -403,7 +402,7 @@ def timed_steps(eng, steps: int, barrier):
     return t1 - t0, per
 
 
-def sustained_loop(eng, states, steps: int, block: int, barrier, dist, dev, n: int, batch_all: int) -> dict:
+def sustained_loop(eng, states, steps: int, block: int, barrier, comm, n: int, batch_all: int) -> dict:
     """SURVEY 8(d)'s sustained rate: the closed loop from the start states (warm state reset) over `steps` HL
     steps, timed per block of `block` steps like the timed region (barrier + device synchronisation around
     one dat_closed_loop call; max over ranks, counters summed).  The late blocks hold the stalled ADMM loops
@@ -428,11 +427,11 @@ def sustained_loop(eng, states, steps: int, block: int, barrier, dist, dev, n: i
                      -w.get("min_env_dist", np.inf), w.get("tail_routed", 0), w.get("certified_infeasible", 0),
                      w.get("stall_exits", 0), w.get("tail_passes", 0), w.get("tail_critical_ipm_iters", 0)])
     rows = np.array(rows, dtype=np.float64)
-    if dist is not None:
+    if comm is not None:
         from distributed_aerial_transportation_amd.sharding import reduce_values
 
-        mx = reduce_values(rows.reshape(-1), "max", dev).reshape(rows.shape)
-        rows = reduce_values(rows.reshape(-1), "sum", dev).reshape(rows.shape)
+        mx = reduce_values(rows.reshape(-1), "max", comm).reshape(rows.shape)
+        rows = reduce_values(rows.reshape(-1), "sum", comm).reshape(rows.shape)
         rows[:, 0], rows[:, 6], rows[:, 8] = mx[:, 0], mx[:, 6], mx[:, 8]
     blocks = []
     b0 = 0
@@ -465,22 +464,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    dist = None
+    comm = None
     if world > 1:
-        import torch
-        import torch.distributed as dist
+        if args.selftest:  # CPU-only check of the launch / shard / combine path: the gloo test harness
+            import torch.distributed as tdist
 
-        if args.selftest:
-            dist.init_process_group("gloo", init_method="env://")
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", init_method="env://")
-    dev = "cpu" if args.selftest else f"cuda:{local}"
+            from tests._gloo_comm import GlooComm
+
+            tdist.init_process_group("gloo", init_method="env://")
+            comm = GlooComm()
+        else:  # RCCL over xGMI through libdat.so (no PyTorch in the rank processes)
+            from distributed_aerial_transportation_amd.sharding import Comm
+
+            comm = Comm.from_env(device=local)
 
     if args.config != "C4":
         if args.selftest:
             sys.exit("bench.py: --selftest covers the C4 path only")
-        return qp_level(args, dist, rank, world, local)
+        return qp_level(args, comm, rank, world, local)
     n = args.n
     total = args.total_batch
     B = args.batch if total is None else strong_shard(rank, world, total)[1]
@@ -502,12 +503,8 @@ def main():
     eng.reset_counters()
 
     def barrier():
-        if dist is not None:
-            if not args.selftest:
-                import torch
-
-                torch.cuda.synchronize()
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()  # (RCCL: every stream of the rank drained first)
 
     elapsed, per_step = timed_steps(eng, args.steps, barrier)
     elapsed_rank0 = elapsed
@@ -524,8 +521,8 @@ def main():
                               (np.asarray(res.qp_status) != 0).sum(axis=1).astype(np.float64)], 1)
     tot = np.array([qps, ipm, hl_ms, elapsed, row_it, work.get("inband_exits", 0), B,
                     work.get("inband_beyond_clarabel_tol", 0)], dtype=np.float64)
-    if dist is not None:
-        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, dev)
+    if comm is not None:
+        sums, maxs, all_metrics = combine_ranks(comm, tot, local_metrics)
         qps_all, ipm_all, row_all = float(sums[0]), float(sums[1]), float(sums[4])
         inband_all, scen_all, loose_all = int(sums[5]), int(sums[6]), int(sums[7])
         elapsed = float(maxs[3])
@@ -536,10 +533,10 @@ def main():
         inband_all, scen_all, loose_all = int(tot[5]), B, int(tot[7])
     sust = None
     if args.sustained_steps > 0 and not args.selftest:
-        sust = sustained_loop(eng, states, args.sustained_steps, args.sustained_block, barrier, dist, dev, n, scen_all)
+        sust = sustained_loop(eng, states, args.sustained_steps, args.sustained_block, barrier, comm, n, scen_all)
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        if comm is not None:
+            comm.close()
         return
     value = qps_all / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -629,11 +626,11 @@ def main():
         out["cpu_baseline"] = cpu_baseline(n, args.cpu_sample_s, args.start, args.forests, args.warmup, args.steps, B,
                                            args.sustained_steps, args.sustained_block)
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
 
 
-def qp_level(args, dist, rank: int, world: int, local: int):
+def qp_level(args, comm, rank: int, world: int, local: int):
     """C2 / C3 / C5: one step = one batched control step of every scenario from HBM-resident states
     (no rollout, no env).  acc_des cycles through ACC_POOL pre-drawn arrays; its host-to-device copy
     (48 B per scenario) is inside the timed region.  Warm state (f, f_bar, lambda / lambda_F,M)
@@ -672,11 +669,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     eng.reset_counters()
 
     def barrier():
-        if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()
 
     barrier()
     eng.synchronize()
@@ -701,15 +695,15 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     local_metrics = np.stack([res.iters.astype(np.float64), res.min_env_dist, res.collision.astype(np.float64),
                               (np.asarray(res.qp_status) != 0).sum(axis=1).astype(np.float64)], 1)
     tot = np.array([w["qp_solves"], w["ipm_iters"], w["hl_kernel_ms"], elapsed, w["ipm_row_iters"]])
-    if dist is not None:
-        sums, maxs, all_metrics = combine_ranks(dist, world, tot, local_metrics, f"cuda:{local}")
+    if comm is not None:
+        sums, maxs, all_metrics = combine_ranks(comm, tot, local_metrics)
         qps, ipm, rows, elapsed = float(sums[0]), float(sums[1]), float(sums[4]), float(maxs[3])
     else:
         all_metrics = local_metrics
         qps, ipm, rows = float(tot[0]), float(tot[1]), float(tot[4])
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        if comm is not None:
+            comm.close()
         return
     # (the QP-level configs have no forest: the C-ADMM drain is the class-0 kernel k_cadmm0)
     kernel = {"cadmm": "k_cadmm0", "dd": "k_dd", "centralized": "k_cent"}.get(args.mode, args.mode)
@@ -750,8 +744,8 @@ def qp_level(args, dist, rank: int, world: int, local: int):
     if not args.no_cpu_baseline and world == 1 and args.qp_tol == 1e-10:
         out["cpu_baseline"] = cpu_baseline_qp(cfg, n, args.mode, args.cpu_sample_s, args.fixed_work)
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
 
 
 if __name__ == "__main__":

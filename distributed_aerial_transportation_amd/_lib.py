@@ -18,13 +18,15 @@ REPO = os.path.dirname(PKG)
 LIB_PATH = os.path.join(PKG, "libdat.so")
 SRC = os.path.join(PKG, "csrc", "dat.hip")
 SRC_CENT = os.path.join(PKG, "csrc", "dat_cent.hip")  # k_cent<n>: its own translation unit, compiled in parallel
+SRC_COMM = os.path.join(PKG, "csrc", "dat_comm.hip")  # RCCL metric collectives (dat_comm_*)
+SRCS = (SRC, SRC_CENT, SRC_COMM)
 OBJ_DIR = os.path.join(PKG, "build")
 # -ffp-contract=on: multiply-adds fused within a source expression only (not across statements, which
 # depends on the inlining context): an inlined function computes the same bits at every call site and in
 # every kernel (k_cadmm / k_cadmm_rob run the same agent-QP passes, dat_qp.hpp).  C4 A/B: k_cadmm 3.53 ->
 # 3.55 ms per step.
 HIPFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=on"]
-DEPS = [SRC, SRC_CENT, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_qp.hpp"),
+DEPS = [SRC, SRC_CENT, SRC_COMM, os.path.join(PKG, "csrc", "dat_core.hpp"), os.path.join(PKG, "csrc", "dat_qp.hpp"),
         os.path.join(PKG, "csrc", "dat_kargs.hpp"), os.path.join(PKG, "csrc", "dat_layout.h"),
         os.path.join(REPO, "include", "dat.h")]
 
@@ -90,9 +92,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if not force and _stamp() == want:  # built by another process while this one waited
             return LIB_PATH
         tag = f"{os.getpid()}"
-        objs = [os.path.join(OBJ_DIR, f"{os.path.basename(src)}.{tag}.o") for src in (SRC, SRC_CENT)]
+        objs = [os.path.join(OBJ_DIR, f"{os.path.basename(src)}.{tag}.o") for src in SRCS]
         tmp_lib = f"{LIB_PATH}.{tag}.tmp"
-        cmds = [["hipcc"] + HIPFLAGS + ["-c", src, "-o", o] for src, o in zip((SRC, SRC_CENT), objs)]
+        cmds = [["hipcc"] + HIPFLAGS + ["-c", src, "-o", o] for src, o in zip(SRCS, objs)]
         procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for c in cmds]
         errs = []
         try:
@@ -108,7 +110,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         try:
             if errs:
                 raise DatError("\n".join(errs))
-            link = ["hipcc"] + HIPFLAGS + ["-shared"] + objs + ["-o", tmp_lib]
+            link = ["hipcc"] + HIPFLAGS + ["-shared"] + objs + ["-lrccl", "-o", tmp_lib]
             r = subprocess.run(link, capture_output=True, text=True)
             if r.returncode != 0:
                 raise DatError("hipcc link failed:\n" + r.stderr[-4000:])
@@ -172,6 +174,13 @@ EXPORTS = {
     "dat_get_agent_qp_ms": (ctypes.c_int, [H, D]),
     "dat_rp_rollout": (ctypes.c_int, [H, ctypes.c_int, D]),
     "dat_low_level_control": (ctypes.c_int, [H, D, D, D]),
+    "dat_comm_unique_id": (ctypes.c_int, [U8]),
+    "dat_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, U8, ctypes.POINTER(H)]),
+    "dat_comm_destroy": (ctypes.c_int, [H]),
+    "dat_comm_allgather": (ctypes.c_int, [H, D, ctypes.c_longlong, D]),
+    "dat_comm_allreduce": (ctypes.c_int, [H, D, ctypes.c_longlong, ctypes.c_int]),
+    "dat_comm_barrier": (ctypes.c_int, [H]),
+    "dat_comm_last_error": (ctypes.c_char_p, []),
 }
 
 

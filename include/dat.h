@@ -239,6 +239,28 @@ int dat_solve_agent_qp_batch(dat_handle* h, int count, const int* scenario, cons
                              const double* lam, const double* rho, const double* f_mean, const double* c9, double* x,
                              int* status, int* ipm_iters, unsigned char* collision, double* min_env_dist);
 
+/* ---- metric collectives of a sharded run (K8) ----------------------------------------------
+ * Scenarios shard over the GPUs of a node with no collective inside the control step; what crosses GPUs is the
+ * per-scenario metrics the reference's loop keeps in its lists (iteration counts, min env distance, collision
+ * flag: example/rqp_example.py:112-138) and the run's work counters.  The reference runs one scenario in one
+ * process and has no such call; these replace the torch.distributed collectives a PyTorch harness would use,
+ * over RCCL (xGMI), with host buffers.  One process per GPU: rank 0 creates the id, the launcher hands it to the
+ * others (sharding.py: a file keyed by the launcher's rendezvous), every rank calls dat_comm_create. */
+#define DAT_COMM_ID_BYTES 128
+#define DAT_COMM_SUM 0
+#define DAT_COMM_MAX 1
+typedef struct dat_comm dat_comm;
+int dat_comm_unique_id(unsigned char* id /* DAT_COMM_ID_BYTES */);
+int dat_comm_create(int device, int nranks, int rank, const unsigned char* id, dat_comm** out);
+int dat_comm_destroy(dat_comm* c);
+/* recv[nranks x count] = every rank's send[count], in rank order */
+int dat_comm_allgather(dat_comm* c, const double* send, long long count, double* recv);
+/* buf[count] = element-wise sum (DAT_COMM_SUM) or max (DAT_COMM_MAX) over the ranks, in place */
+int dat_comm_allreduce(dat_comm* c, double* buf, long long count, int op);
+/* every rank's device work done, then a one-value all-reduce */
+int dat_comm_barrier(dat_comm* c);
+const char* dat_comm_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

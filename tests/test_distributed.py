@@ -1,5 +1,6 @@
 """The multi-GPU path of bench.py on CPU: scenario sharding and the rank-combination step, run over a
-world-size-2 gloo group (the GPU run uses the same functions over RCCL/xGMI, one process per GPU)."""
+world-size-2 gloo group through the test harness's GlooComm (tests/_gloo_comm.py; the GPU run uses the same
+functions over sharding.Comm, RCCL over xGMI through libdat.so, one process per GPU)."""
 
 import os
 import socket
@@ -29,7 +30,9 @@ def _worker(rank, world, port, B, out):
         tot = np.array([100.0 * (rank + 1), 600.0 * (rank + 1), 5.0 + rank, 1.0 + 0.5 * rank, 1800.0 * (rank + 1)])
         sf, seed = bench.shard(rank, B, 64)
         metrics = np.stack([np.full(B, float(rank)), sf.astype(np.float64), np.zeros(B)], 1)
-        sums, maxs, gathered = bench.combine_ranks(dist, world, tot, metrics, "cpu")
+        from tests._gloo_comm import GlooComm
+
+        sums, maxs, gathered = bench.combine_ranks(GlooComm(), tot, metrics)
         if rank == 0:
             np.save(out, np.concatenate([sums, maxs, gathered.reshape(-1), [seed]]))
     finally:
@@ -135,11 +138,14 @@ def _uneven_worker(rank, world, port, total, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from tests._gloo_comm import GlooComm
+
+        comm = GlooComm()
         lo, cnt = shard_range(rank, world, total)
         ids = np.arange(lo, lo + cnt, dtype=np.float64)
-        rows = gather_rows(np.stack([ids, np.full(cnt, float(rank))], 1))
-        s = reduce_values([cnt, 1.0], "sum")
-        m = reduce_values([cnt, rank], "max")
+        rows = gather_rows(np.stack([ids, np.full(cnt, float(rank))], 1), comm)
+        s = reduce_values([cnt, 1.0], "sum", comm)
+        m = reduce_values([cnt, rank], "max", comm)
         if rank == 0:
             np.save(out, np.concatenate([rows.reshape(-1), s, m]))
     finally:

@@ -10,7 +10,8 @@ name=$1; shift
 P=$R/distributed_aerial_transportation_amd
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=on"
 [ -f $R/build_var/dat_cent.o ] || hipcc $F -c $P/csrc/dat_cent.hip -o $R/build_var/dat_cent.o
+[ -f $R/build_var/dat_comm.o ] || hipcc $F -c $P/csrc/dat_comm.hip -o $R/build_var/dat_comm.o
 hipcc $F "$@" -c $P/csrc/dat.hip -o $R/build_var/dat_$name.o
-hipcc $F -shared $R/build_var/dat_$name.o $R/build_var/dat_cent.o -o $R/build_var/libdat_$name.so
+hipcc $F -shared $R/build_var/dat_$name.o $R/build_var/dat_cent.o $R/build_var/dat_comm.o -lrccl -o $R/build_var/libdat_$name.so
 rm -f $R/build_var/dat_$name.o
 echo "built build_var/libdat_$name.so ($*)"
