@@ -30,6 +30,17 @@
 
 using namespace dat;
 
+#ifdef DAT_CAPTURE_LOOSE
+// development builds only (tools/capture_loose.py): the inputs of the tail's agent QPs accepted in band beyond
+// Clarabel's 1e-8 -- [0] scenario, [1] agent, [2] ADMM pass, [3] rho, [4] previous step's passes, [5] forest,
+// [6] merit, [7] fused step, [8, 14) acc_des, then the state (S), the agent's multipliers (3n) and the mean (3n)
+namespace dat {
+constexpr int CAP_MAX = 64, CAP_DOUBLES = 320;
+__device__ double g_cap[CAP_MAX][CAP_DOUBLES];
+__device__ unsigned int g_ncap;
+}  // namespace dat
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -636,6 +647,19 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
             shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane},
             NoGrp{}, wrl, wson);
         wc.stall += o.why == 7;
+#ifdef DAT_CAPTURE_LOOSE
+        if (inband_loose(o)) {
+          const unsigned k = atomicAdd(&g_ncap, 1u);
+          if (k < (unsigned)CAP_MAX && 14 + a.S + 6 * n <= CAP_DOUBLES) {
+            double* c = g_cap[k];
+            c[0] = sc; c[1] = i; c[2] = iter; c[3] = rho; c[4] = prev_iter;
+            c[5] = a.scen_forest ? a.scen_forest[sc] : -1; c[6] = o.merit; c[7] = kstep;
+            for (int q = 0; q < 6; ++q) c[8 + q] = a.acc[((size_t)kstep * a.B + sc) * 6 + q];
+            for (int q = 0; q < a.S; ++q) c[14 + q] = a.state[(size_t)sc * a.S + q];
+            for (int q = 0; q < N3; ++q) { c[14 + a.S + q] = lam[q]; c[14 + a.S + N3 + q] = fb[q]; }
+          }
+        }
+#endif
       } else if constexpr (CLS < NCLS - 1 && (CLS >= ROWLDS_MIN_CLS || AUXM != 0)) {
         if (AUXM != 0 && rmode == 2)
           o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, AUXM, NoGrp, RM>(
@@ -2114,6 +2138,16 @@ int finish_hl(dat_handle* h, int ksteps = 1) {
 
 extern "C" {
 
+#ifdef DAT_CAPTURE_LOOSE
+int dat_get_captures(double* out, int* count) {
+  HIPCHK(hipDeviceSynchronize());
+  unsigned int k = 0;
+  HIPCHK(hipMemcpyFromSymbol(&k, HIP_SYMBOL(dat::g_ncap), sizeof(k)));
+  *count = (int)k;
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(dat::g_cap), sizeof(double) * CAP_MAX * CAP_DOUBLES));
+  return 0;
+}
+#endif
 #ifdef DAT_ITER_HIST
 int dat_get_iter_hist(unsigned long long* out) {
   HIPCHK(hipDeviceSynchronize());

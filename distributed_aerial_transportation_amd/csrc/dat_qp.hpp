@@ -1358,6 +1358,22 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
     bool okc = true;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
+      if (ROB) {
+        // a second-order cone iterate that rounding put on (or past) the boundary: back inside by a few ulps of
+        // its axis (the step rule keeps it strictly inside in exact arithmetic).  Without it the robust solver
+        // stopped at the NT scaling (why 3) on the stall QPs the 10 s C4 loop accepted beyond Clarabel's 1e-8 (20
+        // of 20 captured, tests/golden/ref_loose_caps.npz); with it all 20 converge to 1e-11.
+#pragma unroll
+        for (int b0 = 1; b0 <= 5; b0 += 4) {
+          double* vv[2] = {sk[k] + b0, zk[k] + b0};
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            double* v = vv[q];
+            const double n1 = sqrt(v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);
+            if (!(v[0] - n1 > 1e-14 * n1)) v[0] = n1 * (1.0 + 1e-14) + 1e-300;
+          }
+        }
+      }
       ID0(k) = sqrt(zk[k][0] * frcp(sk[k][0]));  // 1 / d0, d0 = sqrt(s0 / z0)
       LAM(k, 0) = sqrt(sk[k][0] * zk[k][0]);
       okc = okc && soc_scaling(sk[k] + 1, zk[k] + 1, S1[k]) && soc_scaling(sk[k] + 5, zk[k] + 5, S2[k]);

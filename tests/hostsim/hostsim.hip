@@ -176,6 +176,45 @@ int hs_qp_cadmm_warm(const double* prm, int n, const double* st, const double* a
   return o.status;
 }
 
+// one ipm_attempt of the C-ADMM agent QP (development: tools/loose_probe.py): rob selects the robust
+// instantiation, start the initial point (0 conservative, 1 tuned, 2 conservative x 10)
+int hs_qp_cadmm_attempt(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
+                        const double* env_rhs, int nenv, int i, const double* lam, const double* fbar, double rho,
+                        int rob, int start, double* f_out, int* iters) {
+  if (nenv > DAT_NENV) return -1;
+  double Rt_all[16 * 9];
+  const double* Rl = st + DAT_S_RL(n);
+  for (int j = 0; j < n; ++j) make_Rt(prm + DAT_P_RCOM(n) + 3 * j, Rl, Rt_all + 9 * j);
+  QPShared S;
+  build_shared(S, prm, n, st, acc, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
+  QPLane<1> P;
+  lane_cadmm_static(P, prm, i);
+  double lhs[DAT_NENV][3], rhs[DAT_NENV];
+  unsigned mask;
+  env_slots(env_lhs, env_rhs, nenv, lhs, rhs, &mask);
+  EnvRows E;
+  set_env_rows(P, E, S, mask, lhs, rhs);
+  lane_cadmm_dynamic(P, prm, n, i, Rt_all, lam, fbar, rho);
+  double y[1][3], w[6], best[best_size(1)];
+  const PlainRef<QPShared> sh{&S};
+  const EnvPlain er{&E};
+  const RtPtr rt{Rt_all + 9 * i};
+  IPMOut o = rob ? ipm_attempt<MODE_CADMM, 1, DAT_MAXROW, PlainRef<QPShared>, EnvPlain, RtPtr, RowRegs, 0, NoGrp, true>(
+                       sh, er, rt, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50, HS_TOL, RowRegs{}, NoGrp{}, start)
+                 : ipm_attempt<MODE_CADMM, 1, DAT_MAXROW, PlainRef<QPShared>, EnvPlain, RtPtr, RowRegs, 0, NoGrp, false>(
+                       sh, er, rt, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, best, 50, HS_TOL, RowRegs{}, NoGrp{}, start);
+  diag(o);
+  for (int j = 0; j < n; ++j) {
+    if (j == i) {
+      for (int c = 0; c < 3; ++c) f_out[3 * j + c] = y[0][c];
+    } else {
+      cadmm_free_block(Rt_all + 9 * j, lam + 3 * j, fbar + 3 * j, o.pi, rho, f_out + 3 * j);
+    }
+  }
+  *iters = o.iters;
+  return o.status;
+}
+
 int hs_qp_dd(const double* prm, int n, const double* st, const double* acc, const double* env_lhs,
              const double* env_rhs, int nenv, int i, const double* c9, double* x_out, int* iters) {
   if (nenv > DAT_NENV) return -1;
