@@ -37,11 +37,13 @@ constexpr int NBASE = 3;          // base slots shared by all agents of a scenar
 // six to keep the dual residual below the stopping tolerance (tools/hard_qp_probe.py: 2 passes left
 // 281 of 798 such solves at in-band exits, 6 passes 69, all within 1.5e-6 of the oracle)
 constexpr int NREF = 6;
-// The robust instantiation (stiff rows in augmented form) at most two: on the C4 stall stretches (host build,
+// The robust instantiation (stiff rows in augmented form) at most one: on the C4 stall stretches (host build,
 // tools/stall_warm_hostsim.py) its warm-started solves ran 4.75 refinement passes and 4.43 corrections per IPM
 // iteration with six -- most stop at the cap, the residual of the augmented system does not reach the rounding
-// test -- and 1.9 / 1.7 with two, at the same IPM iterations per solve (8.5) and f_des within 1.4e-6 of the oracle
-constexpr int NREF_ROB = 2;
+// test -- 1.9 / 1.7 with two and 1.0 / 0.9 with one, at about the same IPM iterations per solve (8.5, 8.2) and
+// f_des within 1.5e-6 of the oracle.  GPU A/B (tools/r06_ab.sh): the stall stretches alone 48.1 / 36.5 -> 41.6 /
+// 33.2 ms per step, the 10 s loop 36.0 -> 33.0 ms per step on average, 0 accepts beyond 1e-8 either way.
+constexpr int NREF_ROB = 1;
 // Initial point: cone / row slacks shifted to at least IPM_S0 inside, duals IPM_Z0 e.  The agent QPs'
 // multipliers are O(1e-2) at the solution; starting the duals and the slack margins there instead of at 1
 // takes 7.00 -> 5.23 IPM iterations per C-ADMM agent QP on the C4 closed loop (CPU sweep over

@@ -28,7 +28,22 @@ args = ap.parse_args()
 lib = L.lib()
 lib.dat_get_phase_cycles.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 buf = (ctypes.c_ulonglong * 16)()
-if args.config == "C4":
+if args.config == "stall":  # the C4 stall stretches of ref_c4_hard.npz alone (the tail kernel's regime)
+    from distributed_aerial_transportation_amd import Forest
+
+    d = np.load(os.path.join(ROOT, "tests", "golden", "ref_c4_hard.npz"))
+    n, J = 6, d["x0"].shape[0]
+    eng = BatchedController("cadmm", n, J, scenarios.params_block(n))
+    eng.set_forests([Forest.seeded(int(s)) for s in d["forest_seed"]], np.arange(J, dtype=np.int32))
+    eng.set_state(d["x0"], np.zeros(J, dtype=np.int32))
+    for k in range(2):
+        eng.control(None, None)
+        eng.rollout(10)
+    lib.dat_get_phase_cycles(buf)
+    for k in range(args.steps):
+        eng.control(None, None)
+        eng.rollout(10)
+elif args.config == "C4":
     n, B = 6, 65536
     sf, st, forests = bench.bench_states(n, B, 0, 1, 64, "path", None)
     eng = BatchedController("cadmm", n, B, scenarios.params_block(n))
