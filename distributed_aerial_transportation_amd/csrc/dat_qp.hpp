@@ -220,6 +220,8 @@ constexpr int WREC_SIZE = 28 + 2 * DAT_MAXROW;
 // stall, control/rqp_cadmm.py:661 -- or p >= TAIL_PASS).  The GPU runs those passes in k_cadmm_tail (dat.hip).
 // The rule depends on the scenario's own history only, so its results do not depend on the scenarios it is
 // batched with.  Normal C4 steps take 1-14 passes: the warm closed loop never meets it.
+// (TAIL_PASS = 8 measured worse: the warm window's 9-14-pass scenarios then finish after k_cadmm, C4 3.87 -> 4.58
+// ms per step, and the 10 s loop did not gain, 33.0 -> 34.0 ms per step; tools/r06_ab.sh)
 constexpr int TAIL_PREV = 20, TAIL_PASS = 16;
 
 // ------------------------------------------------------------------ shared data
