@@ -124,6 +124,9 @@ def parse():
                     help="after the timed steps: the closed loop from the start states over this many HL steps "
                          "(SURVEY 8(d)'s 10 s), reported per block of --sustained-block steps (stats.sustained); 0: off")
     ap.add_argument("--sustained-block", type=int, default=100)
+    ap.add_argument("--persistent-blocks", type=int, default=0,
+                    help="resident k_cadmm / k_dd workgroups (0: the library default, 4 per CU); more workgroups "
+                         "hold fewer scenario slots each (dat_set_persistent_blocks)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-s", type=float, default=15.0)
     ap.add_argument("--selftest", action="store_true",
@@ -495,6 +498,8 @@ def main():
         scen_forest, states, forests = bench_states(n, B, rank, world, args.forests, args.start, total)
         eng = BatchedController(args.mode, n, B, scenarios.params_block(n), device=local if world > 1 else 0)
         eng.set_qp_tolerance(args.qp_tol)
+        if args.persistent_blocks:
+            eng.set_persistent_blocks(args.persistent_blocks)
         eng.set_forests(forests, scen_forest)
         eng.set_state(states, np.zeros(B, dtype=np.int32))
         if args.sub_batches > 1:
@@ -600,7 +605,7 @@ def main():
         "config": {"workload": workload,
                    "n": n, "scenarios_per_gpu": B, "total_scenarios": scen_all, "hl_every": 10, "dt": 1e-3,
                    "qp_tol": args.qp_tol, "parallelism": f"scenario-sharded x{world}",
-                   "sub_batches": args.sub_batches},
+                   "sub_batches": args.sub_batches, "persistent_blocks": args.persistent_blocks or "default"},
         "stats": {"agent_qp_solves": qps_all, "ipm_iters": ipm_all, "mean_ipm_iters_per_qp": ipm_all / max(qps_all, 1),
                   "mean_active_rows": row_all / max(ipm_all, 1),
                   "mean_admm_iters": float(np.mean(all_metrics[:, 0])), "collisions_last_step": int(all_metrics[:, 2].sum()),
@@ -643,6 +648,8 @@ def qp_level(args, comm, rank: int, world: int, local: int):
     eng = BatchedController(args.mode, n, B, params, per_scenario_params=per_scen,
                             device=local if world > 1 else 0)
     eng.set_qp_tolerance(args.qp_tol)
+    if args.persistent_blocks:
+        eng.set_persistent_blocks(args.persistent_blocks)
     if args.fixed_work:
         eng.set_force_err_tolerance(0.0, False)
         eng.set_max_iter(25)
@@ -729,7 +736,7 @@ def qp_level(args, comm, rank: int, world: int, local: int):
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (perturbed rest states, acc_des ~ U(-5,5)^6" + (", randomized payload mass/inertia)" if per_scen else ")"),
         "config": {"workload": workload, "n": n, "scenarios_per_gpu": B, "qp_tol": args.qp_tol,
-                   "parallelism": f"scenario-sharded x{world}"},
+                   "parallelism": f"scenario-sharded x{world}", "persistent_blocks": args.persistent_blocks or "default"},
         "stats": {"agent_qp_solves": qps, "ipm_iters": ipm, "mean_ipm_iters_per_qp": ipm / max(qps, 1),
                   "mean_active_rows": rows / max(ipm, 1), "mean_admm_iters": float(np.mean(all_metrics[:, 0])),
                   "non_optimal_agent_qps_last_step": int(all_metrics[:, 3].sum()),

@@ -182,6 +182,20 @@ __device__ inline CadmmLds cadmm_carve(double* smem, int n, int G, int cls, int 
   return L;
 }
 
+// order-preserving unsigned key of a double (negative values included) for the running minimum of the env
+// distance (atomicMin on the key): the sign bit flipped for x >= 0, every bit for x < 0
+__host__ __device__ inline unsigned long long dist_key(double x) {
+  unsigned long long b;
+  memcpy(&b, &x, sizeof(b));
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__host__ __device__ inline double dist_of_key(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  double x;
+  memcpy(&x, &b, sizeof(x));
+  return x;
+}
+
 // env class of one agent QP: 0 if it carries no env row, otherwise the smallest class whose slots
 // hold the rows set_env_rows keeps (nonzero rows, compacted).  An all-zero row with a positive
 // right-hand side (0 >= rhs > 0: the reference's QP is infeasible, set_env_rows flags it) also
@@ -410,8 +424,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // longest scenarios are claimed first and scenarios sharing a wavefront tend to need similar
     // numbers of ADMM passes and of IPM iterations per pass (a pass lasts as long as its slowest lane)
     const int bin = NPB * iter_bin(a.iters[sc]) + ipm_bin(a.ipmx[sc]);
-    // a scenario wedged in a stall (previous step > TAIL_PREV passes) goes to the tail (key NKEY + class)
-    a.need[sc] = a.iters[sc] > a.tail_prev ? NKEY + cls : cls * NIB + (NIB - 1 - bin);
+    // a scenario wedged in a stall (previous step > TAIL_PREV passes) goes to the tail (key NKEY + class); with
+    // sub-batches it stays in k_cadmm's queue, which hands it over after its first pass (the tail rule), the
+    // same arithmetic
+    a.need[sc] = a.route && a.iters[sc] > a.tail_prev ? NKEY + cls : cls * NIB + (NIB - 1 - bin);
     a.col[sc] = (unsigned char)c;
     a.mind[sc] = m;
     cnum = c;
@@ -425,9 +441,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
   }
   if (lane == 0) {
     if (cnum) atomicAdd(a.counters + CNT_COLL, (unsigned long long)cnum);
+    // (an order-preserving key of the signed distance: a collided payload's distance is negative)
     unsigned long long* pm = a.counters + CNT_COLL + 1;
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(cmin);
-    if (cmin >= 0.0 && bits < *(volatile unsigned long long*)pm) atomicMin(pm, bits);
+    const unsigned long long key = dist_key(cmin);
+    if (cmin == cmin && key < *(volatile unsigned long long*)pm) atomicMin(pm, key);
   }
 }
 
@@ -628,7 +645,11 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     bool active = slot_sc >= 0;
     int it_lane = 0;
     bool hand = false;  // k_cadmm: this lane's solve was not clean (ipm_unclean)
-    if (active && ((rmask >> i) & 1)) {
+    // k_cadmm with sub-batches (no tail routing, KArgs::route): a wedged scenario leaves before its first pass, and
+    // the tail runs its step from there, as it runs a routed one
+    const bool wedged = !RB && iter == 0 && prev_iter > a.tail_prev;
+    if (active && wedged) hand = true;
+    if (active && !wedged && ((rmask >> i) & 1)) {
       lane_cadmm_dynamic(P, prm, n, i, rts, lam, fb, rho, RT_STRIDE);
       DAT_PHASE(15);
       P.tuned = iter == 0 || prev_iter <= 3;  // see ipm_solve: first pass, or the warm closed-loop regime
@@ -1892,8 +1913,8 @@ struct dat_handle {
   hipEvent_t sub_done[DAT_MAX_SUB] = {};
   hipEvent_t ev_start = nullptr, ev_end = nullptr;
   // C-ADMM with a forest: per sub-batch the stream of the concurrent tail launch and its start / end events
-  hipStream_t tail_stream[DAT_MAX_SUB] = {};
-  hipEvent_t tail_ev[2 * DAT_MAX_SUB] = {};
+  hipStream_t tail_stream = nullptr;  // C-ADMM, one sub-batch: the tail-routed scenarios' launch beside k_cadmm
+  hipEvent_t tail_ev[2] = {};
   double* wrec = nullptr;  // C-ADMM: the tail's warm-start records (B n WREC_SIZE)
   double agent_qp_ms = 0.0;  // device time of the last dat_solve_agent_qp_batch launch
   int ll_kind = 0;  // LL_PD (example/rqp_example.py:113) or LL_SM
@@ -1988,9 +2009,19 @@ KArgs kargs(dat_handle* h) {
   a.wrec = h->wrec;
   a.tail_prev = h->nforest > 0 ? TAIL_PREV : INT_MAX;
   a.tail_pass = h->nforest > 0 ? TAIL_PASS : INT_MAX;
+  // the concurrent tail launch needs a stream of its own beside the step's: with sub-batches (4 streams) a fifth
+  // and more would share the box's GPU_MAX_HW_QUEUES = 4 hardware queues with them and serialise the sub-batches
+  a.route = h->cfg.mode == DAT_MODE_CADMM && h->nforest > 0 && h->nsub == 1;
+  // (created on first use: a stream made at dat_create would take a hardware queue from the sub-batch streams)
+  if (a.route && !h->tail_stream &&
+      (hipStreamCreateWithFlags(&h->tail_stream, hipStreamNonBlocking) != hipSuccess ||
+       hipEventCreateWithFlags(&h->tail_ev[0], hipEventDisableTiming) != hipSuccess ||
+       hipEventCreateWithFlags(&h->tail_ev[1], hipEventDisableTiming) != hipSuccess))
+    a.route = 0;  // (no stream: the wedged scenarios go through k_cadmm's hand-over, same results)
   a.tmode = 0;
 #ifdef DAT_NO_TAIL  // A/B builds only (tools/build_var.sh): the round-5 schedule, no tail rule
   a.tail_prev = a.tail_pass = INT_MAX;
+  a.route = 0;
 #endif
   return a;
 }
@@ -2013,20 +2044,22 @@ size_t dd_setup_lds(int n) {
 // tail stream, started with k_cadmm (their lists are known after k_bucket), and the hand-over lists after
 // k_cadmm on the step's stream, which then waits for the first.
 constexpr int TAIL_BLOCKS = 256;
-int launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st, int sub = 0) {
+int launch_cadmm(const dat_handle* h, const KArgs& a, int blocks, hipStream_t st) {
   KArgs r = a;
   r.G = 1;
   if (h->nforest > 0) {
-    KArgs t = r;
-    t.tmode = 1;
-    const hipStream_t ts = h->tail_stream[sub];
-    HIPCHK(hipEventRecord(h->tail_ev[2 * sub], st));
-    HIPCHK(hipStreamWaitEvent(ts, h->tail_ev[2 * sub], 0));
-    hipLaunchKernelGGL(k_cadmm_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(a.n, NCLS - 1), ts, t);
-    HIPCHK(hipEventRecord(h->tail_ev[2 * sub + 1], ts));
+    if (a.route) {
+      KArgs t = r;
+      t.tmode = 1;
+      const hipStream_t ts = h->tail_stream;
+      HIPCHK(hipEventRecord(h->tail_ev[0], st));
+      HIPCHK(hipStreamWaitEvent(ts, h->tail_ev[0], 0));
+      hipLaunchKernelGGL(k_cadmm_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(a.n, NCLS - 1), ts, t);
+      HIPCHK(hipEventRecord(h->tail_ev[1], ts));
+    }
     hipLaunchKernelGGL(k_cadmm, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, NCLS - 1), st, a);
     hipLaunchKernelGGL(k_cadmm_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(r.n, NCLS - 1), st, r);
-    HIPCHK(hipStreamWaitEvent(st, h->tail_ev[2 * sub + 1], 0));
+    if (a.route) HIPCHK(hipStreamWaitEvent(st, h->tail_ev[1], 0));
   } else {
     hipLaunchKernelGGL(k_cadmm0, dim3(blocks), dim3(64), cadmm_lds_bytes(a.n, a.G, 0), st, a);
     hipLaunchKernelGGL(k_cadmm0_tail, dim3(TAIL_BLOCKS), dim3(64), cadmm_tail_lds_bytes(r.n, 0), st, r);
@@ -2245,11 +2278,6 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->rres, B * RRES_INTS);
     rc |= dalloc(h, &h->rlist, B);
     rc |= dalloc(h, &h->wrec, B * n * WREC_SIZE);
-    for (int s = 0; s < DAT_MAX_SUB && rc == 0; ++s)
-      if (hipStreamCreateWithFlags(&h->tail_stream[s], hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&h->tail_ev[2 * s], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&h->tail_ev[2 * s + 1], hipEventDisableTiming) != hipSuccess)
-        rc = fail("dat_create: tail stream/event creation failed");
   } else if (c.mode == DAT_MODE_DD) {
     rc |= dalloc(h, &h->need, B);
     rc |= dalloc(h, &h->ipmx, B);
@@ -2304,14 +2332,12 @@ int dat_destroy(dat_handle* h) {
     if (h->sub_stream[s]) (void)hipStreamDestroy(h->sub_stream[s]);
     if (h->sub_done[s]) (void)hipEventDestroy(h->sub_done[s]);
   }
-  for (int s = 0; s < DAT_MAX_SUB; ++s) {
-    if (h->tail_stream[s]) {
-      (void)hipStreamSynchronize(h->tail_stream[s]);
-      (void)hipStreamDestroy(h->tail_stream[s]);
-    }
-    if (h->tail_ev[2 * s]) (void)hipEventDestroy(h->tail_ev[2 * s]);
-    if (h->tail_ev[2 * s + 1]) (void)hipEventDestroy(h->tail_ev[2 * s + 1]);
+  if (h->tail_stream) {
+    (void)hipStreamSynchronize(h->tail_stream);
+    (void)hipStreamDestroy(h->tail_stream);
   }
+  for (int e = 0; e < 2; ++e)
+    if (h->tail_ev[e]) (void)hipEventDestroy(h->tail_ev[e]);
   if (h->ev_start) (void)hipEventDestroy(h->ev_start);
   if (h->ev_end) (void)hipEventDestroy(h->ev_end);
   for (hipEvent_t e : h->sub_ev) (void)hipEventDestroy(e);
@@ -2545,7 +2571,7 @@ int closed_loop_sub(dat_handle* h, int hl_steps) {
       hipLaunchKernelGGL(k_bucket, dim3(1), dim3(BUCKET_T), 0, st, Bs, (const int*)a.need, a.slist, a.scount);
       const hipEvent_t* ev = h->sub_ev.data() + 2 * ((size_t)k * S + s);
       HIPCHK(hipEventRecord(ev[0], st));
-      if (launch_cadmm(h, a, std::min((Bs + a.G - 1) / a.G, h->persistent_blocks), st, s)) return -1;
+      if (launch_cadmm(h, a, std::min((Bs + a.G - 1) / a.G, h->persistent_blocks), st)) return -1;
       HIPCHK(hipEventRecord(ev[1], st));
       launch_rollout(a, Bs, st, h->cfg.hl_every, h->cfg.dt, (const double*)a.fdes);
       HIPCHK(hipGetLastError());
@@ -2672,7 +2698,7 @@ int dat_reset_counters(dat_handle* h) {
   HIPCHK(hipSetDevice(h->cfg.device));
   HIPCHK(hipMemsetAsync(h->counters, 0, DAT_NCOUNTERS * sizeof(unsigned long long), h->stream));
   {  // the running minimum of the env distance starts at +inf
-    static const double inf = HUGE_VAL;
+    static const unsigned long long inf = dist_key(HUGE_VAL);
     HIPCHK(hipMemcpyAsync(h->counters + CNT_COLL + 1, &inf, sizeof(inf), hipMemcpyHostToDevice, h->stream));
   }
   h->cadmm_ms = 0.0;
@@ -2896,11 +2922,7 @@ int dat_get_collision_stats(dat_handle* h, long long* collisions, double* min_en
   HIPCHK(hipMemcpyAsync(c, h->counters + CNT_COLL, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   if (collisions) *collisions = (long long)c[0];
-  if (min_env_dist) {
-    double m;
-    memcpy(&m, &c[1], sizeof(m));
-    *min_env_dist = m;
-  }
+  if (min_env_dist) *min_env_dist = dist_of_key(c[1]);
   return 0;
 }
 

@@ -109,6 +109,7 @@ struct KArgs {
                                  // (dat_control_steps; acc then holds ksteps x B x 6 values)
   double* wrec;                  // C-ADMM tail: per agent lane the warm-start record (WREC_SIZE doubles)
   int tail_prev, tail_pass;      // C-ADMM: the tail rule (TAIL_PREV / TAIL_PASS with a forest, INT_MAX without)
+  int route;                     // C-ADMM, one sub-batch: wedged scenarios go to the tail before the step (k_env_class)
   int tmode;                     // k_cadmm_tail: 0 the hand-over lists (rlist), 1 the tail-routed stretch of slist
 };
 

@@ -208,8 +208,9 @@ int dat_get_robust_redos(dat_handle* h, long long* redos);
  * reference call. */
 int dat_get_tail_counters(dat_handle* h, long long* out);
 /* C-ADMM with a forest: scenario-steps with a collision flag and the smallest minimum env distance over every
- * HL step since the last counter reset (the reference logs min_env_dist per step and flags a collision below
- * its threshold: example/rqp_example.py:129, example/env_forest.py:158-159; +inf without a forest). */
+ * HL step since the last counter reset, signed (negative once a body is inside a tree: the reference logs
+ * min_env_dist per step and flags a collision below its threshold: example/rqp_example.py:129,
+ * example/env_forest.py:158-159; +inf without a forest). */
 int dat_get_collision_stats(dat_handle* h, long long* collisions, double* min_env_dist);
 /* Device time [ms] of the last dat_solve_agent_qp_batch launch (k_agent_qp; HIP events on the handle's
  * stream): the solve_time RQPPrimalSolver.solve returns (Clarabel's solver_stats.solve_time,

@@ -69,5 +69,11 @@ def test_gpu_c4_collision_replay():
             assert np.array_equal(r.collision, d["collision"][k]), k
             assert np.max(np.abs(r.f_des - ref)) / max(1.0, np.max(np.abs(ref))) < 1e-9, k
             eng.rollout(10)
+        # the device counters of the same steps (bench stats.sustained): collided scenario-steps and the signed
+        # smallest env distance (negative: inside the tree)
+        w = eng.work()
+        assert w["collisions"] == int(d["collision"].sum())
+        assert w["min_env_dist"] == pytest.approx(float(d["min_env_dist"].min()), abs=1e-9)
+        assert w["min_env_dist"] < 0.0
     finally:
         eng.close()
