@@ -190,8 +190,10 @@ constexpr int IPM_NSTIFF = 8;
 DAT_HD constexpr int best_rec(int NB) { return 3 * NB + 18; }
 DAT_HD constexpr int stiff_col(int NB) { return 3 * NB + 12; }
 constexpr int STIFF_ROW = 8;  // a0 a1 a2 on_dwl e g dz tmp
+// (and, last, FM_DOUBLES for the warm-start instantiation's u-space factor P: ipm_attempt WS)
+constexpr int FM_DOUBLES = 21;
 DAT_HD constexpr int best_size(int NB) {
-  return best_rec(NB) + IPM_NSTIFF * (stiff_col(NB) + STIFF_ROW) + IPM_NSTIFF * (IPM_NSTIFF + 1) / 2;
+  return best_rec(NB) + IPM_NSTIFF * (stiff_col(NB) + STIFF_ROW) + IPM_NSTIFF * (IPM_NSTIFF + 1) / 2 + FM_DOUBLES;
 }
 // Clarabel's own tolerance: an in-band exit whose merit is above it is one Clarabel would not certify
 constexpr double IPM_CLARABEL_TOL = 1e-8;
@@ -1457,7 +1459,12 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
     double* const hcol = best + best_rec(NB);                    // [j][dy (3 NB), dw (6), du (6)]
     double* const srec = hcol + IPM_NSTIFF * stiff_col(NB);      // [j][a0 a1 a2 on_dwl e g dz tmp]
     double* const sfac = srec + IPM_NSTIFF * STIFF_ROW;          // Cholesky factor of S
-    double Lm[21];  // DD: Cholesky factor of M;  CADMM / CENT: P = Lm N^-1 Lm' (schur_P)
+    // DD: Cholesky factor of M;  CADMM / CENT: P = Lm N^-1 Lm' (schur_P).  WS (the tail kernel, one scenario
+    // per workgroup, latency-bound): kept in the lane's scratch record (LDS there) across the iteration's solves
+    // instead of 42 registers of a frame that spills (stall fixture, same-call A/B: 41.8 / 33.7 -> 39.1 / 30.6 ms per
+    // stalled step; the cones' s, z and the Newton step's cone terms there as well measured no better, or worse)
+    double LmR[21];
+    double* const Lm = WS ? best + best_size(NB) - FM_DOUBLES : LmR;
     {
       double Mm[21];
       // M = C + sum_l (z/s) a_l a_l' (u-space, packed), assembled in (dvl, dwl) coordinates
