@@ -5,7 +5,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$R/gpurun_out/prof
+OUT=${OUT:-$R/gpurun_out/prof}
 mkdir -p $OUT
 B=${B:-65536}
 # B=default: the bench's own default workload (65,536 scenarios, strong split), whose workload string
