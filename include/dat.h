@@ -144,7 +144,11 @@ int dat_closed_loop(dat_handle* h, int hl_steps);
 /* C-ADMM handles: run dat_closed_loop on `count` (1..4) contiguous sub-batches of the scenarios, each on
  * its own stream with no synchronisation between sub-batches or steps, so that one sub-batch's kernels
  * fill the others' drain tails and short kernels.  Per scenario the arithmetic is unchanged (a scenario's
- * results never depend on the grouping).  count = 1 (default) restores the single-stream loop. */
+ * results never depend on the grouping).  count = 1 (default) restores the single-stream loop.  With a forest
+ * and count = 1 the scenarios wedged in a stall (previous step > TAIL_PREV ADMM passes) run in the tail kernel
+ * on a second stream beside the drain; with count > 1 (no further stream: the device's hardware queues are
+ * shared by all streams) the drain hands them to the tail kernel before their first pass -- the same passes,
+ * the same results. */
 int dat_set_sub_batches(dat_handle* h, int count);
 /* Host steady-clock marks (ms) of the last dat_closed_loop call: [0] its start (0.0), then the completion
  * of each HL step's control kernel; consecutive differences are per-step times of the back-to-back run.
