@@ -151,6 +151,12 @@ __host__ __device__ inline size_t cadmm_lds_bytes(int n, int G, int max_cls = NC
 // dynamic LDS of a k_cadmm_tail workgroup (one scenario slot, rmode 3), with the n lanes' IPM scratch records
 // (best iterate, stiff-row columns and Schur factor: best_size(1) doubles each) behind the class's area: the
 // robust solver's stiff-row loops read and write them at every iteration, an LDS round trip instead of L2 / HBM
+// k_cadmm_tail: bit-identical clones per agent lane (the lanes a one-scenario wavefront leaves idle), one per
+// stiff-row column of the robust solver at most
+__host__ __device__ inline int tail_clones(int n) {
+  const int v = 64 / (n > 0 ? n : 1);
+  return v < 1 ? 1 : v < IPM_NSTIFF ? v : IPM_NSTIFF;
+}
 __host__ __device__ inline size_t cadmm_tail_lds_bytes(int n, int max_cls = NCLS - 1) {
   size_t m = 0;
   for (int c = 0; c <= max_cls; ++c) {
@@ -529,9 +535,15 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   constexpr int NE = class_env_rows(CLS);
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int n = a.n, N3 = 3 * n;
-  const int G = a.G, NT = G * n;  // G <= 64 / n scenario slots (cadmm_slots)
+  const int G = a.G;  // G <= 64 / n scenario slots (cadmm_slots); the tail: G = 1
+  // the tail: V bit-identical clones of each agent lane (clone vi = lane / n) run the agent QP's solve in lockstep
+  // and share out its stiff-row columns (ipm_attempt); only clone 0 writes the scenario's outputs
+  const int V = RB ? tail_clones(n) : 1;
+  const int NT = (RB ? V : G) * n;
   const int lane = threadIdx.x;
-  const int ls = lane / n, i = lane - ls * n;
+  const int vi = RB ? lane / n : 0;
+  const int ls = RB ? 0 : lane / n, i = lane - (RB ? vi : ls) * n;
+  const int al = RB ? i : lane;  // the lane's column in the row / env / aux images (a clone's: its agent's)
   const int lsc = ls < G ? ls : 0;
   const bool TM = RB && a.tmode == 1;  // the tail-routed stretch of slist (k_env_class), not the hand-over list
   const int first = TM ? a.scount[6 * NCLS + CLS] : a.scount[NCLS + CLS];
@@ -546,7 +558,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   double* myred = L.red + lane * RDS;
   QPShared& S = L.sh[lsc];
   const LdsRef<QPShared> shr{L.sh, lsc};
-  const EnvLdsN<NE> err{L.env, lane};
+  const EnvLdsN<NE> err{L.env, al};
   const RtLds rtr{L.Rt, (lsc * n + i) * RT_STRIDE};
   if (lane < G) L.sid[lane] = -1;
   __syncthreads();
@@ -569,7 +581,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
   for (;;) {
     // ---- refill empty slots from the queue
     DAT_PHASE(11);
-    if (lane < NT && i == 0 && L.sid[ls] == -1) {
+    if (lane < NT && i == 0 && vi == 0 && L.sid[ls] == -1) {
       const int q = atomicAdd(qh, 1);
       const int s2 = q < cnt ? ql[q] : -2;  // -2: queue drained, slot retires
       L.sid[ls] = s2;
@@ -583,11 +595,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       sc = slot_sc;
       prm = prm_of(a, sc);
       const double* st = a.state + (size_t)sc * a.S;
-      make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
+      if (vi == 0) make_Rt(prm + DAT_P_RCOM(n) + 3 * i, st + DAT_S_RL(n), rts + RT_STRIDE * i);
       lam = a.clam + ((size_t)sc * n + i) * N3;
       cfs = a.cf + (size_t)sc * n * N3;
       myf = cfs + i * N3;
-      for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
+      if (vi == 0)
+        for (int c = 0; c < 3; ++c) fb[3 * i + c] = a.cfbar[(size_t)sc * N3 + 3 * i + c];
       // (the tail: the lane's record in LDS, behind the env image -- a generic pointer, flat loads go to LDS)
       bst = RB ? L.env + env_lds_doubles(NE) + i * best_size(1) : a.best + ((size_t)sc * n + i) * best_rec(1);
       iter = 0;
@@ -609,7 +622,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         for (int q = 0; q < iter; ++q) rho = fmin(rho * a.tau, a.rho_max);  // the pass's rho, as k_cadmm had it
         qstat = a.qstatus[(size_t)sc * n + i];  // the pass's status of a lane not solved again
       }
-      if (i == 0)
+      if (i == 0 && vi == 0)
         build_shared(S, prm, n, st, a.acc + ((size_t)kstep * a.B + sc) * 6, prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
     }
     if (!__syncthreads_or(slot_sc >= 0)) break;  // every slot retired
@@ -631,12 +644,12 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         }
         EnvRows E;
         set_env_rows(P, E, S, emask, lhs, rhs);
-        env_to_lds<NE>(L.env, lane, E);
+        env_to_lds<NE>(L.env, al, E);  // (clones: the same values to the same column)
         // the tail certifies infeasible rows once per scenario-step (such an agent QP would run 2 x 50 IPM
         // iterations in every pass and end INACCURATE: the previous solution is held either way)
         if (RB && !P.infeasible && dvl_rows_infeasible(shr, err, P.emask)) {
           P.infeasible = 1;
-          ++wc.cert;
+          wc.cert += vi == 0;
         }
       }
     }
@@ -663,13 +676,13 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       if constexpr (RB) {
         // the tail rule: warm start and stall exit in pass iter (the record is kept in every pass)
         const bool wson = iter >= 1 && (prev_iter > a.tail_prev || iter >= a.tail_pass);
-        wc.warm += wson && wrl[0] == 1.0;
+        wc.warm += vi == 0 && wson && wrl[0] == 1.0;
         o = ipm_solve<MODE_CADMM, 1, NR, SHT, ERT, RtLds, RowLds, TAIL_AUXM, NoGrp, RM, true>(
-            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, lane},
-            NoGrp{}, wrl, wson);
-        wc.stall += o.why == 7;
+            shr, err, rtr, P, prm + DAT_P_FEQ(n) + 3 * i, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowLds{L.rows, al},
+            NoGrp{}, wrl, wson, vi, V);
+        wc.stall += vi == 0 && o.why == 7;
 #ifdef DAT_CAPTURE_LOOSE
-        if (inband_loose(o)) {
+        if (vi == 0 && inband_loose(o)) {
           const unsigned k = atomicAdd(&g_ncap, 1u);
           if (k < (unsigned)CAP_MAX && 14 + a.S + 6 * n <= CAP_DOUBLES) {
             double* c = g_cap[k];
@@ -699,7 +712,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       DAT_PHASE(9);
       // a solve k_cadmm hands over is counted once, by k_cadmm_tail (its IPM_FAST_REDO runs the fast attempt
       // again): its discarded outcome here is neither an agent-QP solve nor an in-band accept
-      const int keep = hand ? 0 : 1;  // (nor do its iterations enter the pass's slot counts)
+      const int keep = hand || vi > 0 ? 0 : 1;  // (nor do its iterations enter the pass's slot counts; nor a clone's)
       wc.ipm += keep * o.iters;
       wc.inband += keep * o.inband;
 #ifdef DAT_ITER_HIST
@@ -712,7 +725,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       wc.rowit += (long long)(keep * o.iters) * (__builtin_popcount(S.bmask) + __builtin_popcount(P.emask));
       wc.qp += keep;
       qstat = o.status;
-      if (o.status == ST_OPTIMAL) {
+      if (vi > 0) {
+      } else if (o.status == ST_OPTIMAL) {
         for (int j = 0; j < n; ++j) {
           if (j == i) {
             myf[3 * j] = y[0][0]; myf[3 * j + 1] = y[0][1]; myf[3 * j + 2] = y[0][2];
@@ -763,7 +777,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       for (int c = 0; c < 3; ++c) myred[c] = s3[c] / n;
     }
     __syncthreads();
-    if (active) {
+    if (active && vi == 0) {
       for (int c = 0; c < 3; ++c) fb[3 * i + c] = myred[c];
     }
     __syncthreads();
@@ -800,7 +814,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
       }
     }
     __syncthreads();
-    if (active && i == 0) {
+    if (active && i == 0 && vi == 0) {
       double res = 0.0;
       const double* rg = L.red + (ls * n) * RDS;
       if (a.use_total_res) {
@@ -822,7 +836,8 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
     __syncthreads();
     if (active) {
       if (!L.done[ls]) {
-        for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
+        if (vi == 0)
+          for (int c = 0; c < N3; ++c) lam[c] += rho * (myf[c] - fb[c]);  // control/rqp_cadmm.py:627-629
         if (!RB && iter >= 1 && (prev_iter > a.tail_prev || iter >= a.tail_pass)) {
           // the tail rule holds from the next pass on: k_cadmm_tail resumes the scenario there (all lanes solve;
           // the mean of this pass goes with it, multipliers and copies are in place)
@@ -840,18 +855,20 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
         }
       } else {
         // the scenario stopped: write its outputs and free the slot
-        if (RB && i == 0) {  // a scenario-step the tail finished (and, routed before the step, counted apart)
+        if (RB && i == 0 && vi == 0) {  // a scenario-step the tail finished (and, routed before the step, apart)
           atomicAdd(a.counters + CNT_ROB, 1ull);
           if (TM && kstep == 0) atomicAdd(a.counters + CNT_TAIL + 2, 1ull);
         }
-        for (int c = 0; c < 3; ++c) {
-          a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
-          a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
-        }
-        a.qstatus[(size_t)sc * n + i] = qstat;
-        if (i == 0) {
-          a.iters[sc] = iter;
-          a.ipmx[sc] = L.wmx[ls];
+        if (vi == 0) {
+          for (int c = 0; c < 3; ++c) {
+            a.cfbar[(size_t)sc * N3 + 3 * i + c] = fb[3 * i + c];
+            a.fdes[(size_t)sc * N3 + 3 * i + c] = myf[3 * i + c];  // f_app = diag copies (:669-671)
+          }
+          a.qstatus[(size_t)sc * n + i] = qstat;
+          if (i == 0) {
+            a.iters[sc] = iter;
+            a.ipmx[sc] = L.wmx[ls];
+          }
         }
         if (kstep + 1 < a.ksteps) {
           // fused steps: the scenario's next control step in the same slot (warm f, f_mean, lambda kept;
@@ -862,7 +879,7 @@ __device__ __forceinline__ void cadmm_drain(const KArgs& a) {
           qstat = ST_OPTIMAL;
           rho = a.rho0;
           if (RB) wrl[0] = 0.0;
-          if (i == 0) {
+          if (i == 0 && vi == 0) {
             build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
                          prm[DAT_P_KFD], prm[DAT_P_KMD], 3, true);
             L.wmx[ls] = 0;

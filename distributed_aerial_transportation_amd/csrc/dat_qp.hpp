@@ -843,7 +843,7 @@ template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW, unsi
 DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P,
                                                           const double* y0,
                           double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw, GRP grp,
-                          int start, double* wrec = nullptr, bool wson = false) {
+                          int start, double* wrec = nullptr, bool wson = false, int clone = 0, int nclone = 1) {
   static_assert(NR >= NBASE && NR <= DAT_MAXROW, "row slots");
   // aux slot offsets (only the AUXM groups are allocated)
   constexpr int O_SC = 0;
@@ -1781,8 +1781,10 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
       if (__builtin_expect(!corr && nst > 0, 0)) {
         // the predictor's call first solves for the iteration's stiff-row columns H abar_j (bk = 0,
         // Rf = 0, bu = abar_j) and factors their Schur complement
+        // (k_cadmm_tail: the agent lane's nclone bit-identical clones take every nclone-th column, into the
+        // agent's shared scratch record in LDS; the Schur factorisation below reads all of them)
 #pragma unroll 1
-        for (int j = 0; j < nst; ++j) {
+        for (int j = clone; j < nst; j += nclone) {
           double ab[6];
           {
             const double* r = srec + j * STIFF_ROW;
@@ -1803,6 +1805,12 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
 #pragma unroll
           for (int q = 0; q < 6; ++q) { h[3 * NB + q] = cw[q]; h[3 * NB + 6 + q] = cu[q]; }
         }
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (nclone > 1) {  // the other clones' columns: stores complete before the reads below (one wavefront)
+          __builtin_amdgcn_s_waitcnt(0);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
+#endif
         // Cholesky of the symmetrised Schur complement S, column by column
 #pragma unroll 1
         for (int j = 0; j < nst; ++j) {
@@ -2169,7 +2177,7 @@ template <int MODE, int NB, int NR, class SH, class ER, class RT, class RW = Row
           class GRP = NoGrp, int ROBUST = IPM_FAST, bool WS = false>
 DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<NB>& P, const double* y0,
                         double y[NB][3], double w[6], double* best, int max_iter, double tol, RW rw = RW{},
-                        GRP grp = GRP{}, double* wrec = nullptr, bool wson = false) {
+                        GRP grp = GRP{}, double* wrec = nullptr, bool wson = false, int clone = 0, int nclone = 1) {
   if constexpr (ROBUST == IPM_FAST_REDO) {
     // trip 0 fast; trip 1 robust (the fast outcome not clean); trip 2 fast once more when the robust outcome
     // is worse (deterministic: it reproduces the first; keeping the first iterate instead would hold another
@@ -2184,10 +2192,10 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
       if (WS && wrec && trip == 2) wrec[0] = wflag;
       if (trip == 1 || (wson && wflag == 1.0))  // a warm first trip (and its rerun, trip 2) runs the robust solver
         o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_ROBUST, WS>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                               tol, rw, grp, wrec, wson);
+                                                                               tol, rw, grp, wrec, wson, clone, nclone);
       else
         o = ipm_solve<MODE, NB, NR, SH, ER, RT, RW, AUXM, GRP, IPM_FAST_R, WS>(sh, er, rt, P, y0, y, w, best, max_iter,
-                                                                               tol, rw, grp, wrec, wson);
+                                                                               tol, rw, grp, wrec, wson, clone, nclone);
       o.iters += done;
       o.refs += done_refs;
       o.corrs += done_corrs;
@@ -2233,7 +2241,7 @@ DAT_HD IPMOut ipm_solve(const SH& sh, const ER& er, const RT& rt, const QPLane<N
           sh, er, rt, P, y0, y, w, best,
           start == 3 ? (max_iter > WS_MAXIT ? WS_MAXIT : max_iter)
                      : start == 1 && trip != 1 && max_iter > 20 ? 20 : max_iter,
-          tol, rw, grp, start, wrec, wson);
+          tol, rw, grp, start, wrec, wson, clone, nclone);
       o.iters += done;
       o.refs += done_refs;
       o.corrs += done_corrs;
