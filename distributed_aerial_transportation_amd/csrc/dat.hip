@@ -92,6 +92,18 @@ int fail(const std::string& m) {
 // which with the 256 B of static LDS left room for three workgroups per CU (one SIMD idle); four fit after
 // the trim (C4 A/B 3.83 / 3.80 -> 3.72 / 3.77 ms per step), and the budget then went to classes 1 and 2's
 // aux groups at three per CU instead (LDS_WAVE_BUDGET).
+// DD warm start: from DD pass DD_WARM_PASS of a step on, the agent QPs start from the previous pass's iterate (a
+// long DD chain -- C3's slowest scenario runs the reference's cap of 100 passes at every step, the step's
+// critical path; ordinary steps take ~4 passes and never reach it).  Its agent QP differs from the previous pass's
+// only in the prices.  From pass 1 on it cut C3 further but left the n = 3 golden DD error sequence (25 fixed
+// passes) 3e-4 off (bound 1e-4): a warm start lands elsewhere in a weakly convex QP's near-flat minimiser set than
+// the reference's cold solve.  Same-call A/B (C3, ms per step): 21.7 -> 13.4 with DD_WS_MU 1e-3 (1e-2: 14.3);
+// every DD parity test green (golden sequences, the DD hard stretch, the 100 s loop to the same horizon).
+// (DAT_DD_WARM=0: the round-5 cold DD, A/B builds.)
+#ifndef DAT_DD_WARM
+#define DAT_DD_WARM 1
+#endif
+constexpr int DD_WARM_PASS = 30;
 constexpr int RDS = 7;  // consensus exchange slots per lane: mean (3) or F / M totals (6), total residual at [6]
 // LDS budget of one k_cadmm workgroup: 53 KB = three per CU.  Four per CU (40 KB) bought ~2 % (§5 of
 // DESIGN.md, round 4); the 13 KB more per workgroup hold classes 1 and 2's IPM aux groups in LDS
@@ -1311,6 +1323,7 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
   const double* prm = nullptr;
   const double* Rl = nullptr;
   double* bst = nullptr;
+  double* wrl = nullptr;  // DAT_DD_WARM: the agent QP's warm-start record (HBM)
   double prev[9];
   int sc = -1, iter = 0, qstat = ST_OPTIMAL, col = 0;
   int kstep = 0;  // fused control steps (dat_control_steps): the slot scenario's current step
@@ -1344,6 +1357,10 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       for (int c = 0; c < 9; ++c) prev[c] = a.dprev[((size_t)sc * n + i) * 9 + c];
       for (int c = 0; c < 9; ++c) myX[c] = prev[c];  // the controller's current (f, F, M)
       bst = a.best + ((size_t)sc * n + i) * best_rec(1);
+#if DAT_DD_WARM
+      wrl = a.wrec + ((size_t)sc * n + i) * WREC_SIZE;
+      wrl[0] = 0.0;
+#endif
       iter = 0;
       qstat = ST_OPTIMAL;
       kstep = 0;
@@ -1390,12 +1407,24 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
       IPMOut o;
       const double* y0 = prm + DAT_P_FEQ(n) + 3 * i;
       DAT_PHASE(10);
+#if DAT_DD_WARM
+      // a DD pass after the first: the agent QP differs from the previous pass's only in its prices, so it starts
+      // from that pass's last iterate (ipm_solve WS, the tail kernel's warm start)
+      const bool wson = iter >= DD_WARM_PASS;
+      if constexpr (ENV)
+        o = ipm_solve_rows<MODE_DD, 1, IPM_FAST, true>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, a.qp_tol,
+                                                       wrl, wson);
+      else
+        o = ipm_solve<MODE_DD, 1, NBASE, LdsRef<QPShared>, EnvLds, RtLds, RowRegs, 0, NoGrp, IPM_FAST, true>(
+            shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER, a.qp_tol, RowRegs{}, NoGrp{}, wrl, wson);
+#else
       if constexpr (ENV)
         o = ipm_solve_rows<MODE_DD, 1>(nr, shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                        a.qp_tol);
       else
         o = ipm_solve<MODE_DD, 1, NBASE>(shr, err, rtr, P, y0, y, w, bst, IPM_MAX_ITER,
                                          a.qp_tol);
+#endif
       DAT_PHASE(9);
       my_ipm += o.iters;
       my_inband += o.inband;
@@ -1518,6 +1547,9 @@ __global__ __launch_bounds__(64) void k_dd(KArgs a) {
           // lambda_F, lambda_M and previous solutions it leaves (control/rqp_dd.py:695-700)
           ++kstep;
           iter = 0;
+#if DAT_DD_WARM
+          wrl[0] = 0.0;
+#endif
           qstat = ST_OPTIMAL;
           if (i == 0) {
             build_shared(S, prm, n, a.state + (size_t)sc * a.S, a.acc + ((size_t)kstep * a.B + sc) * 6,
@@ -2303,6 +2335,9 @@ int dat_create(const dat_config* cfg, dat_handle** out) {
     rc |= dalloc(h, &h->dlamF, B * N3);
     rc |= dalloc(h, &h->dlamM, B * N3);
     rc |= dalloc(h, &h->dprev, B * n * 9);
+#if DAT_DD_WARM
+    rc |= dalloc(h, &h->wrec, B * n * WREC_SIZE);
+#endif
     rc |= dalloc(h, &h->dHinv, B * 36 * n * n);
   } else {
     rc |= dalloc(h, &h->pf, B * N3);

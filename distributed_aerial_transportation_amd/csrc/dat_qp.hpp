@@ -211,6 +211,9 @@ constexpr double IPM_CLARABEL_TOL = 1e-8;
 // the smallest f_des difference.
 constexpr double WS_MU = 1e2;
 constexpr int WS_MAXIT = 30;
+// the DD agent QPs' warm-start floor (dat.hip DD_WARM_PASS): better scaled than a stalled C-ADMM loop's, they take
+// a far smaller push (C3: 1e2 19.0, 1e0 14.0, 1e-2 11.2, 1e-3 10.7, 1e-4 11.0 ms per step warm from pass 1)
+constexpr double DD_WS_MU = 1e-3;
 // stall exit of the tail kernel's solves (ipm_attempt WS): best in-band merit <= WS_STALL_TOL and not halved
 // in WS_STALL_ITS iterations
 constexpr double WS_STALL_TOL = 1e-9;
@@ -1095,12 +1098,13 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
   if constexpr (WS) {
     static_assert(NB == 1 && NR <= DAT_MAXROW, "warm start: C-ADMM agent QP");
     if (start == 3) {
-      // (s, z) -> (s + d, z + d) with (s + d)(z + d) >= WS_MU
+      // (s, z) -> (s + d, z + d) with (s + d)(z + d) >= mu (WS_MU; DD_WS_MU for the DD agent QPs)
+      constexpr double mu = MODE == MODE_DD ? DD_WS_MU : WS_MU;
       auto push = [](double s, double z) -> double {
         const double p = s * z;
-        if (!(p < WS_MU)) return 0.0;
+        if (!(p < mu)) return 0.0;
         const double t = s + z;
-        return 0.5 * (sqrt(t * t + 4.0 * (WS_MU - p)) - t);
+        return 0.5 * (sqrt(t * t + 4.0 * (mu - p)) - t);
       };
 #pragma unroll
       for (int c = 0; c < 3; ++c) y[0][c] = wrec[1 + c];
@@ -1468,7 +1472,7 @@ DAT_HD __attribute__((always_inline)) IPMOut ipm_attempt(const SH& sh, const ER&
     // instead of 42 registers of a frame that spills (stall fixture, same-call A/B: 41.8 / 33.7 -> 39.1 / 30.6 ms per
     // stalled step; the cones' s, z and the Newton step's cone terms there as well measured no better, or worse)
     double LmR[21];
-    double* const Lm = WS ? best + best_size(NB) - FM_DOUBLES : LmR;
+    double* const Lm = WS && MODE == MODE_CADMM ? best + best_size(NB) - FM_DOUBLES : LmR;  // (DD: HBM records)
     {
       double Mm[21];
       // M = C + sum_l (z/s) a_l a_l' (u-space, packed), assembled in (dvl, dwl) coordinates
